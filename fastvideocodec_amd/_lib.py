@@ -1,0 +1,82 @@
+"""ctypes binding of libfvc.so (the C-ABI in include/fvc.h).
+
+The product path has exactly one compute backend: these HIP kernels. If the shared
+library is missing or fails to load, every op raises — there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libfvc.so")
+
+c_int = ctypes.c_int
+c_float = ctypes.c_float
+c_size_t = ctypes.c_size_t
+vp = ctypes.c_void_p
+
+# name -> (restype, argtypes)
+_SIGS = {
+    "fvc_version": (c_int, []),
+    "fvc_device_arch_ok": (c_int, []),
+    "fvc_conv_wpack_floats": (c_size_t, [c_int, c_int, c_int, c_int, c_int]),
+    "fvc_conv_pack_weight": (c_int, [vp, vp, c_int, c_int, c_int, c_int, c_int]),
+    "fvc_conv2d_nhwc_f32": (c_int, [vp, vp, vp, vp, vp] + [c_int] * 10 + [vp]),
+    "fvc_deconv2d_nhwc_f32": (c_int, [vp, vp, vp, vp, vp] + [c_int] * 10 + [vp]),
+    "fvc_nchw_to_nhwc": (c_int, [vp, vp, c_int, c_int, c_int, c_int, c_int, vp]),
+    "fvc_nhwc_to_nchw": (c_int, [vp, vp, c_int, c_int, c_int, c_int, c_int, c_int, vp]),
+    "fvc_avgpool2_nhwc": (c_int, [vp, vp, c_int, c_int, c_int, c_int, vp]),
+    "fvc_warp_nhwc": (c_int, [vp, vp, vp, c_int, c_int, c_int, c_int, vp]),
+    "fvc_upsample2x_add_nhwc": (c_int, [vp, vp, vp, c_int, c_int, c_int, c_int, c_int, c_float, vp]),
+    "fvc_spynet_assemble": (c_int, [vp, vp, vp, vp, vp, c_int, c_int, c_int, vp]),
+    "fvc_mc_assemble": (c_int, [vp, vp, vp, vp, c_int, c_int, c_int, vp]),
+    "fvc_sub_f32": (c_int, [vp, vp, vp, c_size_t, vp]),
+    "fvc_gdn_nhwc": (c_int, [vp, vp, vp, vp, c_int, c_int, c_int, c_int, c_int, vp]),
+    "fvc_reduce_ws_doubles": (c_size_t, []),
+    "fvc_recon_finalize": (c_int, [vp] * 7 + [c_int, c_int, c_int, vp]),
+    "fvc_bits_laplace": (c_int, [vp] * 4 + [c_int] * 5 + [vp]),
+    "fvc_bits_factorized": (c_int, [vp] * 4 + [c_int] * 5 + [vp]),
+    "fvc_latent_to_symbols": (c_int, [vp, vp] + [c_int] * 5 + [vp]),
+    "fvc_symbols_to_latent": (c_int, [vp, vp] + [c_int] * 5 + [vp]),
+    "fvc_build_indexes": (c_int, [vp, vp, c_int, vp] + [c_int] * 5 + [vp]),
+    "fvc_channel_indexes": (c_int, [vp, c_int, c_int, c_int, vp]),
+    "fvc_pmf_to_quantized_cdf": (c_int, [vp, c_int, c_int, vp]),
+    "fvc_rans_encode": (c_int, [vp, vp, vp, c_int, vp, c_int, vp, vp, vp, vp, vp, vp]),
+    "fvc_rans_pack": (c_int, [vp, vp, vp, c_int, vp, vp, vp]),
+    "fvc_rans_decode": (c_int, [vp, vp, vp, vp, c_int, vp, c_int, vp, vp, vp, vp, vp]),
+}
+
+EXPORTED = tuple(_SIGS)
+
+_lib = None
+_err = None
+
+
+class FvcError(RuntimeError):
+    pass
+
+
+def load():
+    """Load libfvc.so (once). Raises FvcError if it is missing or lacks a symbol."""
+    global _lib, _err
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise FvcError(f"libfvc.so not built at {LIB_PATH}; run __graft_entry__.build() "
+                       "(no CPU fallback exists for the codec path)")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(lib, name)  # AttributeError if a symbol is missing
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def call(name, *args):
+    """Call a status-returning entry point; raise on a non-zero status."""
+    st = getattr(load(), name)(*args)
+    if st != 0:
+        raise FvcError(f"{name} failed with status {st}")
+    return st

@@ -1,0 +1,375 @@
+// Entropy-coding kernels: latent <-> symbol streams, scale-table indexes, and a batched
+// device rANS coder that is byte-compatible, stream for stream, with compressai's
+// RansEncoder/RansDecoder.{encode,decode}_with_indexes (ryg_rans 64-bit state, 32-bit words,
+// precision 16, 4-bit bypass for escapes), the C++ coder the reference reaches through
+// entropy_models.py:80-94 (RecProbModel.compress/decompress).
+//
+// Parallelism: one lane per independent stream (a stream = one channel of one latent of one
+// frame); a stream's symbol loop is inherently sequential (rANS state chain).
+#include "fvc_common.h"
+
+namespace {
+
+constexpr int kBlk = 256;
+constexpr uint64_t kRansL = 1ull << 31;
+constexpr int kPrec = 16;
+constexpr int kBypassPrec = 4;
+constexpr int kMaxBypass = (1 << kBypassPrec) - 1;
+
+__global__ void k_latent_to_symbols(const float* __restrict__ lat, int32_t* __restrict__ sym, int B, int HW, int C,
+                                    int cp) {
+  const size_t n = (size_t)B * C * HW;
+  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < n; e += (size_t)gridDim.x * blockDim.x) {
+    const size_t i = e % HW;
+    const size_t bc = e / HW;
+    const size_t c = bc % C, b = bc / C;
+    sym[e] = (int32_t)rintf(lat[(b * HW + i) * cp + c]);
+  }
+}
+
+__global__ void k_symbols_to_latent(const int32_t* __restrict__ sym, float* __restrict__ lat, int B, int HW, int C,
+                                    int cp) {
+  const size_t n = (size_t)B * HW * cp;
+  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < n; e += (size_t)gridDim.x * blockDim.x) {
+    const int c = e % cp;
+    const size_t p = e / cp;
+    const size_t b = p / HW, i = p % HW;
+    lat[e] = c < C ? (float)sym[(b * C + c) * HW + i] : 0.f;
+  }
+}
+
+// compressai GaussianConditional.build_indexes: s = max(scale, 0.11);
+// idx = (n-1) - #{t in table[:-1] : s <= t}
+__global__ void k_build_indexes(const float* __restrict__ sigma, const float* __restrict__ table, int nt,
+                                int32_t* __restrict__ idx, int B, int HW, int C, int cp) {
+  const size_t n = (size_t)B * C * HW;
+  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < n; e += (size_t)gridDim.x * blockDim.x) {
+    const size_t i = e % HW;
+    const size_t bc = e / HW;
+    const size_t c = bc % C, b = bc / C;
+    const float s = fmaxf(sigma[(b * HW + i) * cp + c], 0.11f);
+    int v = nt - 1;
+    for (int k = 0; k < nt - 1; ++k) v -= (s <= table[k]) ? 1 : 0;
+    idx[e] = v;
+  }
+}
+
+__global__ void k_channel_indexes(int32_t* __restrict__ idx, int B, int HW, int C) {
+  const size_t n = (size_t)B * C * HW;
+  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < n; e += (size_t)gridDim.x * blockDim.x)
+    idx[e] = (int32_t)((e / HW) % C);
+}
+
+// ---- ryg_rans 64-bit primitives (rans64.h) + compressai bypass extension
+__device__ __forceinline__ bool enc_put(uint64_t& x, uint32_t*& ptr, const uint32_t* lo, uint32_t start,
+                                        uint32_t freq) {
+  const uint64_t x_max = ((kRansL >> kPrec) << 32) * freq;
+  if (x >= x_max) {
+    if (ptr <= lo) return false;
+    *--ptr = (uint32_t)x;
+    x >>= 32;
+  }
+  x = ((x / freq) << kPrec) + (x % freq) + start;
+  return true;
+}
+
+__device__ __forceinline__ bool enc_put_bits(uint64_t& x, uint32_t*& ptr, const uint32_t* lo, uint32_t val) {
+  const uint32_t freq = 1u << (16 - kBypassPrec);
+  const uint64_t x_max = ((kRansL >> 16) << 32) * freq;
+  if (x >= x_max) {
+    if (ptr <= lo) return false;
+    *--ptr = (uint32_t)x;
+    x >>= 32;
+  }
+  x = (x << kBypassPrec) | val;
+  return true;
+}
+
+__global__ void k_rans_encode(const int32_t* __restrict__ symbols, const int32_t* __restrict__ indexes,
+                              const int64_t* __restrict__ sym_off, int nstreams, const int32_t* __restrict__ cdfs,
+                              int cdf_stride, const int32_t* __restrict__ cdf_sizes,
+                              const int32_t* __restrict__ offsets, uint32_t* __restrict__ words,
+                              const int64_t* __restrict__ word_off, int32_t* __restrict__ nwords) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= nstreams) return;
+  uint32_t* const lo = words + word_off[s];
+  uint32_t* const hi = words + word_off[s + 1];
+  uint32_t* ptr = hi;
+  uint64_t x = kRansL;
+  bool ok = true;
+  // Symbols are pushed forward (main symbol, then bypass count nibbles, then raw nibbles) and
+  // flushed backward; walking the stream backward and each symbol's sub-symbols in reverse
+  // push order reproduces that flush exactly.
+  for (int64_t i = sym_off[s + 1] - 1; ok && i >= sym_off[s]; --i) {
+    const int32_t ci = indexes[i];
+    const int32_t* cdf = cdfs + (size_t)ci * cdf_stride;
+    const int32_t max_value = cdf_sizes[ci] - 2;
+    int32_t value = symbols[i] - offsets[ci];
+    uint32_t raw = 0;
+    if (value < 0) {
+      raw = (uint32_t)(-2 * value - 1);
+      value = max_value;
+    } else if (value >= max_value) {
+      raw = (uint32_t)(2 * (value - max_value));
+      value = max_value;
+    }
+    if (value == max_value) {
+      int32_t nb = 0;
+      while (nb < 8 && (raw >> (nb * kBypassPrec)) != 0) ++nb;
+      for (int32_t j = nb - 1; ok && j >= 0; --j) ok = enc_put_bits(x, ptr, lo, (raw >> (j * kBypassPrec)) & kMaxBypass);
+      // count nibbles: pushed as kMaxBypass x q then r ; flushed as r then kMaxBypass x q
+      const int32_t q = nb / kMaxBypass, r = nb - q * kMaxBypass;
+      if (ok) ok = enc_put_bits(x, ptr, lo, (uint32_t)r);
+      for (int32_t k = 0; ok && k < q; ++k) ok = enc_put_bits(x, ptr, lo, kMaxBypass);
+    }
+    if (ok) ok = enc_put(x, ptr, lo, (uint32_t)cdf[value], (uint32_t)(cdf[value + 1] - cdf[value]));
+  }
+  if (ok && ptr - lo >= 2) {
+    ptr -= 2;
+    ptr[0] = (uint32_t)x;
+    ptr[1] = (uint32_t)(x >> 32);
+    nwords[s] = (int32_t)(hi - ptr);
+  } else {
+    nwords[s] = -1;
+  }
+}
+
+__global__ void k_pack_scan(const int32_t* __restrict__ nwords, int n, int64_t* __restrict__ pack_off) {
+  // single block, fixed-order exclusive scan
+  __shared__ int64_t part[kBlk];
+  const int per = (n + kBlk - 1) / kBlk;
+  const int b0 = threadIdx.x * per;
+  int64_t s = 0;
+  for (int i = b0; i < b0 + per && i < n; ++i) s += nwords[i] > 0 ? nwords[i] : 0;
+  part[threadIdx.x] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int64_t run = 0;
+    for (int t = 0; t < kBlk; ++t) {
+      const int64_t v = part[t];
+      part[t] = run;
+      run += v;
+    }
+    pack_off[n] = run;
+  }
+  __syncthreads();
+  int64_t run = part[threadIdx.x];
+  for (int i = b0; i < b0 + per && i < n; ++i) {
+    pack_off[i] = run;
+    run += nwords[i] > 0 ? nwords[i] : 0;
+  }
+}
+
+__global__ void k_pack_copy(const uint32_t* __restrict__ words, const int64_t* __restrict__ word_off,
+                            const int32_t* __restrict__ nwords, const int64_t* __restrict__ pack_off,
+                            uint32_t* __restrict__ out) {
+  const int s = blockIdx.x;
+  const int32_t n = nwords[s];
+  if (n <= 0) return;
+  const uint32_t* src = words + word_off[s + 1] - n;
+  uint32_t* dst = out + pack_off[s];
+  for (int i = threadIdx.x; i < n; i += blockDim.x) dst[i] = src[i];
+}
+
+__device__ __forceinline__ bool dec_renorm(uint64_t& x, const uint32_t*& ptr, const uint32_t* end) {
+  if (x < kRansL) {
+    if (ptr >= end) return false;
+    x = (x << 32) | *ptr++;
+  }
+  return true;
+}
+
+__global__ void k_rans_decode(const uint32_t* __restrict__ packed, const int64_t* __restrict__ pack_off,
+                              const int32_t* __restrict__ indexes, const int64_t* __restrict__ sym_off, int nstreams,
+                              const int32_t* __restrict__ cdfs, int cdf_stride, const int32_t* __restrict__ cdf_sizes,
+                              const int32_t* __restrict__ offsets, int32_t* __restrict__ symbols,
+                              int32_t* __restrict__ status) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= nstreams) return;
+  const uint32_t* ptr = packed + pack_off[s];
+  const uint32_t* end = packed + pack_off[s + 1];
+  bool ok = end - ptr >= 2;
+  uint64_t x = 0;
+  if (ok) {
+    x = (uint64_t)ptr[0] | ((uint64_t)ptr[1] << 32);
+    ptr += 2;
+  }
+  const uint64_t mask = (1ull << kPrec) - 1;
+  for (int64_t i = sym_off[s]; i < sym_off[s + 1]; ++i) {
+    if (!ok) {
+      symbols[i] = 0;
+      continue;
+    }
+    const int32_t ci = indexes[i];
+    const int32_t* cdf = cdfs + (size_t)ci * cdf_stride;
+    const int32_t size = cdf_sizes[ci];
+    const int32_t max_value = size - 2;
+    const uint32_t cum = (uint32_t)(x & mask);
+    int lo = 0, hi = size - 1;  // cdf[lo] <= cum < cdf[hi]
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if ((uint32_t)cdf[mid] <= cum) lo = mid; else hi = mid;
+    }
+    const uint32_t start = (uint32_t)cdf[lo], freq = (uint32_t)(cdf[lo + 1] - cdf[lo]);
+    x = freq * (x >> kPrec) + (x & mask) - start;
+    ok = dec_renorm(x, ptr, end);
+    int32_t value = lo;
+    if (ok && value == max_value) {
+      auto getbits = [&](int32_t& v) {
+        v = (int32_t)(x & kMaxBypass);
+        x >>= kBypassPrec;
+        return dec_renorm(x, ptr, end);
+      };
+      int32_t v = 0;
+      ok = getbits(v);
+      int32_t nb = v;
+      while (ok && v == kMaxBypass && nb < 64) {
+        ok = getbits(v);
+        nb += v;
+      }
+      if (nb > 8) ok = false;
+      uint32_t raw = 0;
+      for (int32_t j = 0; ok && j < nb; ++j) {
+        ok = getbits(v);
+        raw |= (uint32_t)v << (j * kBypassPrec);
+      }
+      value = (int32_t)(raw >> 1);
+      if (raw & 1) value = -value - 1;
+      else value += max_value;
+    }
+    symbols[i] = value + offsets[ci];
+  }
+  status[s] = ok ? 0 : FVC_ECORRUPT;
+}
+
+static int grid_for(size_t n) {
+  size_t g = (n + kBlk - 1) / kBlk;
+  if (g > 8192) g = 8192;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+}  // namespace
+
+extern "C" {
+
+int fvc_latent_to_symbols(const float* lat, int32_t* sym, int batch, int h, int w, int c, int cp, fvc_stream_t s) {
+  if (!lat || !sym || c > cp) return FVC_EINVAL;
+  const size_t n = (size_t)batch * c * h * w;
+  hipLaunchKernelGGL(k_latent_to_symbols, dim3(grid_for(n)), dim3(kBlk), 0, (hipStream_t)s, lat, sym, batch, h * w,
+                     c, cp);
+  FVC_CHECK_LAUNCH();
+  return 0;
+}
+
+int fvc_symbols_to_latent(const int32_t* sym, float* lat, int batch, int h, int w, int c, int cp, fvc_stream_t s) {
+  if (!lat || !sym || c > cp) return FVC_EINVAL;
+  const size_t n = (size_t)batch * cp * h * w;
+  hipLaunchKernelGGL(k_symbols_to_latent, dim3(grid_for(n)), dim3(kBlk), 0, (hipStream_t)s, sym, lat, batch, h * w,
+                     c, cp);
+  FVC_CHECK_LAUNCH();
+  return 0;
+}
+
+int fvc_build_indexes(const float* sigma, const float* table, int nt, int32_t* idx, int batch, int h, int w, int c,
+                      int cp, fvc_stream_t s) {
+  if (!sigma || !table || !idx || nt < 1 || c > cp) return FVC_EINVAL;
+  const size_t n = (size_t)batch * c * h * w;
+  hipLaunchKernelGGL(k_build_indexes, dim3(grid_for(n)), dim3(kBlk), 0, (hipStream_t)s, sigma, table, nt, idx, batch,
+                     h * w, c, cp);
+  FVC_CHECK_LAUNCH();
+  return 0;
+}
+
+int fvc_channel_indexes(int32_t* idx, int batch, int hw, int c, fvc_stream_t s) {
+  if (!idx) return FVC_EINVAL;
+  const size_t n = (size_t)batch * c * hw;
+  hipLaunchKernelGGL(k_channel_indexes, dim3(grid_for(n)), dim3(kBlk), 0, (hipStream_t)s, idx, batch, hw, c);
+  FVC_CHECK_LAUNCH();
+  return 0;
+}
+
+int fvc_rans_encode(const int32_t* symbols, const int32_t* indexes, const int64_t* sym_off, int nstreams,
+                    const int32_t* cdfs, int cdf_stride, const int32_t* cdf_sizes, const int32_t* offsets,
+                    uint32_t* words, const int64_t* word_off, int32_t* nwords, fvc_stream_t s) {
+  if (!symbols || !indexes || !sym_off || !cdfs || !cdf_sizes || !offsets || !words || !word_off || !nwords ||
+      nstreams <= 0)
+    return FVC_EINVAL;
+  const int blk = 64;
+  hipLaunchKernelGGL(k_rans_encode, dim3((nstreams + blk - 1) / blk), dim3(blk), 0, (hipStream_t)s, symbols, indexes,
+                     sym_off, nstreams, cdfs, cdf_stride, cdf_sizes, offsets, words, word_off, nwords);
+  FVC_CHECK_LAUNCH();
+  return 0;
+}
+
+int fvc_rans_pack(const uint32_t* words, const int64_t* word_off, const int32_t* nwords, int nstreams,
+                  int64_t* pack_off, uint32_t* out, fvc_stream_t s) {
+  if (!words || !word_off || !nwords || !pack_off || !out || nstreams <= 0) return FVC_EINVAL;
+  hipLaunchKernelGGL(k_pack_scan, dim3(1), dim3(kBlk), 0, (hipStream_t)s, nwords, nstreams, pack_off);
+  FVC_CHECK_LAUNCH();
+  hipLaunchKernelGGL(k_pack_copy, dim3(nstreams), dim3(kBlk), 0, (hipStream_t)s, words, word_off, nwords, pack_off,
+                     out);
+  FVC_CHECK_LAUNCH();
+  return 0;
+}
+
+int fvc_rans_decode(const uint32_t* packed, const int64_t* pack_off, const int32_t* indexes, const int64_t* sym_off,
+                    int nstreams, const int32_t* cdfs, int cdf_stride, const int32_t* cdf_sizes,
+                    const int32_t* offsets, int32_t* symbols, int32_t* status, fvc_stream_t s) {
+  if (!packed || !pack_off || !indexes || !sym_off || !cdfs || !cdf_sizes || !offsets || !symbols || !status ||
+      nstreams <= 0)
+    return FVC_EINVAL;
+  const int blk = 64;
+  hipLaunchKernelGGL(k_rans_decode, dim3((nstreams + blk - 1) / blk), dim3(blk), 0, (hipStream_t)s, packed, pack_off,
+                     indexes, sym_off, nstreams, cdfs, cdf_stride, cdf_sizes, offsets, symbols, status);
+  FVC_CHECK_LAUNCH();
+  return 0;
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------------------ host: CDF quantisation
+// compressai cpp_exts/ops/ops.cpp pmf_to_quantized_cdf (called by EntropyModel._pmf_to_cdf).
+// Table build happens once per weight load (EntropyBottleneck/GaussianConditional.update),
+// on the host in the reference too.
+#include <cmath>
+#include <vector>
+
+extern "C" int fvc_pmf_to_quantized_cdf(const float* pmf, int n, int precision, uint32_t* cdf_out) {
+  if (!pmf || !cdf_out || n <= 0 || precision <= 0 || precision > 16) return FVC_EINVAL;
+  for (int i = 0; i < n; ++i)
+    if (pmf[i] < 0 || !std::isfinite(pmf[i])) return FVC_EINVAL;
+  std::vector<uint32_t> cdf(n + 1);
+  cdf[0] = 0;
+  for (int i = 0; i < n; ++i) cdf[i + 1] = (uint32_t)std::round(pmf[i] * (float)(1 << precision));
+  int acc = 0;  // std::accumulate(..., 0) accumulates in int
+  for (int i = 0; i <= n; ++i) acc += (int)cdf[i];
+  const uint32_t total = (uint32_t)acc;
+  if (total == 0) return FVC_EINVAL;
+  for (int i = 0; i <= n; ++i) cdf[i] = (uint32_t)(((uint64_t)(1 << precision) * cdf[i]) / total);
+  for (int i = 1; i <= n; ++i) cdf[i] += cdf[i - 1];
+  cdf[n] = 1u << precision;
+  for (int i = 0; i < n; ++i) {
+    if (cdf[i] == cdf[i + 1]) {
+      uint32_t best_freq = ~0u;
+      int best_steal = -1;
+      for (int j = 0; j < n; ++j) {
+        const uint32_t freq = cdf[j + 1] - cdf[j];
+        if (freq > 1 && freq < best_freq) {
+          best_freq = freq;
+          best_steal = j;
+        }
+      }
+      if (best_steal < 0) return FVC_EINVAL;
+      if (best_steal < i) {
+        for (int j = best_steal + 1; j <= i; ++j) cdf[j]--;
+      } else {
+        for (int j = i + 1; j <= best_steal; ++j) cdf[j]++;
+      }
+    }
+  }
+  for (int i = 0; i < n; ++i)
+    if (cdf[i + 1] <= cdf[i]) return FVC_EINVAL;
+  for (int i = 0; i <= n; ++i) cdf_out[i] = cdf[i];
+  return 0;
+}

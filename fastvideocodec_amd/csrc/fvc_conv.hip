@@ -1,0 +1,410 @@
+// Implicit-GEMM convolution / transposed convolution on fp32 MFMA (v_mfma_f32_32x32x2_f32).
+//
+// Replaces the ATen conv2d / conv_transpose2d calls of the reference DVC forward
+// (DVC/subnet/endecoder.py:142-169 MEBasic 7x7, :228-296 Warp_net/ResBlock 3x3,
+// analysis_mv.py / synthesis_mv.py 3x3 (s2), analysis.py / synthesis.py / analysis_prior.py /
+// synthesis_prior.py 5x5 s2 / 3x3).
+//
+// GEMM view: M = output pixels, N = output channels, K = taps x input channels.
+//  * activations NHWC fp32, channels padded to 4 (cp);
+//  * a block owns TH = 4*WM output rows x 32 output columns ("strips" of 32 pixels, one per
+//    MFMA M-tile) and WN*32 output channels; 4 waves stacked vertically, each WM strips x WN
+//    N-tiles (WM*WN accumulators of 16 VGPRs);
+//  * K is walked in "k-blocks" = (tap, 4 consecutive input channels). One MFMA quad (4 x
+//    32x32x2) consumes two k-blocks: lanes 0-31 take k-block 2q, lanes 32-63 take 2q+1, and
+//    instruction e of the quad uses element e of each lane's float4 (a fixed permutation of the
+//    K order shared by A and B, so results are deterministic);
+//  * the input halo tile of one channel chunk (CC channels) lives in LDS (row stride padded so
+//    CS/4 is odd: conflict-free ds_read_b128 across the 32 pixels of a strip); the packed weights
+//    stream from L2 straight to VGPRs (16 B per lane, 1 KB per wave instruction, coalesced),
+//    software-pipelined one quad ahead together with the LDS reads;
+//  * transposed convs are split into stride^2 output-parity classes, each a stride-1 conv over
+//    the input with a subset of taps (blockIdx.z = batch*classes + class); no zero-insertion.
+//  * epilogue: bias, activation (ReLU / LeakyReLU 0.1), residual add, exp; pad channels = 0.
+#include "fvc_common.h"
+
+namespace {
+
+constexpr int kMaxTaps = 49;
+constexpr int kThreads = 256;
+
+struct ConvArgs {
+  const float* x;
+  const float* w;
+  const float* bias;
+  const float* res;
+  float* y;
+  int B, H, W, cinp;       // input tensor
+  int Ho, Wo, coutp, cout; // output tensor
+  int Hq, Wq;              // virtual output grid (per class)
+  int sin;                 // input step per virtual-grid step
+  int sout;                // output step per virtual-grid step
+  int nclass;
+  int nchunks;
+  int ntp;                 // padded N-tiles in the weight pack (cdiv(coutp,32))
+  int dymin, dxmin;        // halo origin offset (union over classes)
+  int ir, ic;              // halo tile rows / cols
+  int in_op, act, post_op;
+  int kbc[4];              // k-blocks per chunk per class (even)
+  int ntaps[4];
+  int oy0[4], ox0[4];
+  long long wcls[4];       // float offset of each class in the weight pack
+  short tdy[4][kMaxTaps];
+  short tdx[4][kMaxTaps];
+};
+
+template <int CC>
+struct ChunkGeom {
+  static constexpr int CC4 = CC / 4;
+  static constexpr int CS = (CC4 % 2 == 1) ? CC : CC + 4;  // LDS pixel stride (floats)
+};
+
+template <int CC, int WM, int WN>
+__global__ __launch_bounds__(kThreads) void conv_mfma_f32_kernel(const ConvArgs a) {
+  using G = ChunkGeom<CC>;
+  constexpr int CC4 = G::CC4;
+  constexpr int CS = G::CS;
+  constexpr int TH = 4 * WM;
+  constexpr int TW = 32;
+
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  int* tap_off = reinterpret_cast<int*>(smem);  // kMaxTaps ints (64 reserved)
+  float* tile = smem + 64;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int li = lane & 31;
+  const int lh = lane >> 5;
+
+  const int cls = blockIdx.z % a.nclass;
+  const int b = blockIdx.z / a.nclass;
+  const int tiles_x = (a.Wq + TW - 1) / TW;
+  const int qy0 = (blockIdx.x / tiles_x) * TH;
+  const int qx0 = (blockIdx.x % tiles_x) * TW;
+  const int nt0 = blockIdx.y * WN;
+  const int ntaps = a.ntaps[cls];
+  const int kbc = a.kbc[cls];
+
+  if (tid < ntaps) {
+    tap_off[tid] = ((a.tdy[cls][tid] - a.dymin) * a.ic + (a.tdx[cls][tid] - a.dxmin)) * CS;
+  }
+
+  f32x16 acc[WM][WN];
+#pragma unroll
+  for (int m = 0; m < WM; ++m)
+#pragma unroll
+    for (int n = 0; n < WN; ++n)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[m][n][r] = 0.f;
+
+  const int iy0 = qy0 * a.sin + a.dymin;
+  const int ix0 = qx0 * a.sin + a.dxmin;
+  const int tile_elems = a.ir * a.ic * CC4;
+  const float* xb = a.x + (size_t)b * a.H * a.W * a.cinp;
+
+  // per-lane LDS base of each strip pixel (row = wave*WM+m, col = li)
+  int pix_base[WM];
+#pragma unroll
+  for (int m = 0; m < WM; ++m) pix_base[m] = (((wave * WM + m) * a.sin) * a.ic + li * a.sin) * CS;
+
+  const float* wcls = a.w + a.wcls[cls];
+  const int nq = kbc >> 1;
+
+  for (int ch = 0; ch < a.nchunks; ++ch) {
+    // ---- stage the input halo tile of this channel chunk (zero padded, in_op applied)
+    for (int e = tid; e < tile_elems; e += kThreads) {
+      const int c4 = e % CC4;
+      const int p = e / CC4;
+      const int r = p / a.ic;
+      const int c = p - r * a.ic;
+      const int iy = iy0 + r;
+      const int ix = ix0 + c;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (iy >= 0 && iy < a.H && ix >= 0 && ix < a.W) {
+        v = *reinterpret_cast<const float4*>(xb + ((size_t)iy * a.W + ix) * a.cinp + ch * CC + c4 * 4);
+        v = fvc_apply_in_op4(v, a.in_op);
+      }
+      *reinterpret_cast<float4*>(tile + p * CS + c4 * 4) = v;
+    }
+    __syncthreads();
+
+    const float* wch = wcls + (size_t)ch * kbc * a.ntp * 128;
+    float4 A[WM], Bv[WN], An[WM], Bn[WN];
+    auto load = [&](int q, float4 (&Ar)[WM], float4 (&Br)[WN]) {
+      const int kb = 2 * q + lh;
+      const int t = kb / CC4;
+      const int c4 = kb - t * CC4;
+      const int toff = (t < ntaps ? tap_off[t] : 0) + c4 * 4;
+#pragma unroll
+      for (int m = 0; m < WM; ++m) Ar[m] = *reinterpret_cast<const float4*>(tile + pix_base[m] + toff);
+      const float* wk = wch + ((size_t)kb * a.ntp + nt0) * 128 + li * 4;
+#pragma unroll
+      for (int n = 0; n < WN; ++n) Br[n] = *reinterpret_cast<const float4*>(wk + n * 128);
+    };
+    load(0, A, Bv);
+    for (int q = 0; q < nq; ++q) {
+      if (q + 1 < nq) load(q + 1, An, Bn);
+#pragma unroll
+      for (int m = 0; m < WM; ++m)
+#pragma unroll
+        for (int n = 0; n < WN; ++n) {
+          acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x2f32(A[m].x, Bv[n].x, acc[m][n], 0, 0, 0);
+          acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x2f32(A[m].y, Bv[n].y, acc[m][n], 0, 0, 0);
+          acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x2f32(A[m].z, Bv[n].z, acc[m][n], 0, 0, 0);
+          acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x2f32(A[m].w, Bv[n].w, acc[m][n], 0, 0, 0);
+        }
+#pragma unroll
+      for (int m = 0; m < WM; ++m) A[m] = An[m];
+#pragma unroll
+      for (int n = 0; n < WN; ++n) Bv[n] = Bn[n];
+    }
+    __syncthreads();
+  }
+
+  // ---- epilogue
+  const int oy0 = a.oy0[cls], ox0 = a.ox0[cls];
+#pragma unroll
+  for (int n = 0; n < WN; ++n) {
+    const int j = (nt0 + n) * 32 + li;
+    if (j >= a.coutp) continue;
+    const bool real = j < a.cout;
+    const float bj = real ? a.bias[j] : 0.f;
+#pragma unroll
+    for (int m = 0; m < WM; ++m) {
+      const int qy = qy0 + wave * WM + m;
+      if (qy >= a.Hq) continue;
+      const int oy = qy * a.sout + oy0;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int pi = (r & 3) + 8 * (r >> 2) + 4 * lh;
+        const int qx = qx0 + pi;
+        if (qx >= a.Wq) continue;
+        const int ox = qx * a.sout + ox0;
+        const size_t o = (((size_t)b * a.Ho + oy) * a.Wo + ox) * a.coutp + j;
+        float v = acc[m][n][r] + bj;
+        if (a.act == FVC_ACT_RELU) v = v > 0.f ? v : 0.f;
+        else if (a.act == FVC_ACT_LRELU) v = v > 0.f ? v : 0.1f * v;
+        if (a.res) v += a.res[o];
+        if (a.post_op == FVC_POST_EXP) v = expf(v);
+        a.y[o] = real ? v : 0.f;
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------ host-side geometry
+struct Cfg {
+  int cinp, coutp, ntp, cc, wm, wn, nclass, nchunks;
+  int sin, sout;
+  int ntaps[4], kbc[4], oy0[4], ox0[4];
+  int tky[4][kMaxTaps], tkx[4][kMaxTaps];  // kernel tap (ky,kx)
+  int tdy[4][kMaxTaps], tdx[4][kMaxTaps];  // input offsets
+  int dymin, dymax, dxmin, dxmax;
+  long long wcls[4];
+  long long wtotal;
+};
+
+static int floordiv(int a, int b) { return (a >= 0) ? a / b : -((-a + b - 1) / b); }
+
+static bool make_cfg(int cin, int cout, int ks, int stride, int transposed, Cfg& c) {
+  if (cin <= 0 || cout <= 0 || (ks != 1 && ks != 3 && ks != 5 && ks != 7) || (stride != 1 && stride != 2))
+    return false;
+  c.cinp = fvc_rup(cin, 4);
+  c.coutp = fvc_rup(cout, 4);
+  c.ntp = fvc_cdiv(c.coutp, 32);
+  if (c.ntp > 4) return false;
+  const int pad = ks / 2;
+  if (!transposed) {
+    c.nclass = 1;
+    c.sin = stride;
+    c.sout = 1;
+    c.ntaps[0] = 0;
+    for (int ky = 0; ky < ks; ++ky)
+      for (int kx = 0; kx < ks; ++kx) {
+        int t = c.ntaps[0]++;
+        c.tky[0][t] = ky; c.tkx[0][t] = kx;
+        c.tdy[0][t] = ky - pad; c.tdx[0][t] = kx - pad;
+      }
+    c.oy0[0] = c.ox0[0] = 0;
+  } else {
+    c.nclass = stride * stride;
+    c.sin = 1;
+    c.sout = stride;
+    for (int py = 0; py < stride; ++py)
+      for (int px = 0; px < stride; ++px) {
+        const int cl = py * stride + px;
+        c.ntaps[cl] = 0;
+        c.oy0[cl] = py; c.ox0[cl] = px;
+        for (int ky = 0; ky < ks; ++ky) {
+          if (((py + pad - ky) % stride + stride) % stride) continue;
+          for (int kx = 0; kx < ks; ++kx) {
+            if (((px + pad - kx) % stride + stride) % stride) continue;
+            int t = c.ntaps[cl]++;
+            c.tky[cl][t] = ky; c.tkx[cl][t] = kx;
+            c.tdy[cl][t] = floordiv(py + pad - ky, stride);
+            c.tdx[cl][t] = floordiv(px + pad - kx, stride);
+          }
+        }
+      }
+  }
+  c.dymin = c.dxmin = 1 << 20;
+  c.dymax = c.dxmax = -(1 << 20);
+  for (int cl = 0; cl < c.nclass; ++cl)
+    for (int t = 0; t < c.ntaps[cl]; ++t) {
+      c.dymin = c.tdy[cl][t] < c.dymin ? c.tdy[cl][t] : c.dymin;
+      c.dymax = c.tdy[cl][t] > c.dymax ? c.tdy[cl][t] : c.dymax;
+      c.dxmin = c.tdx[cl][t] < c.dxmin ? c.tdx[cl][t] : c.dxmin;
+      c.dxmax = c.tdx[cl][t] > c.dxmax ? c.tdx[cl][t] : c.dxmax;
+    }
+  c.wn = c.ntp;
+  c.wm = (!transposed && stride == 2) ? 1 : 2;
+  // channel chunk: largest of {32,16,8,4} dividing cinp whose halo tile fits 64 KB
+  int cc = 32;
+  for (;; cc >>= 1) {
+    if (cc == 4) break;
+    if (c.cinp % cc) continue;
+    const int TH = 4 * c.wm;
+    const int ir = (TH - 1) * c.sin + 1 + (c.dymax - c.dymin);
+    const int ic = 31 * c.sin + 1 + (c.dxmax - c.dxmin);
+    const int cs = ((cc / 4) % 2 == 1) ? cc : cc + 4;
+    if ((size_t)ir * ic * cs * 4 + 256 <= 64 * 1024) break;
+  }
+  c.cc = cc;
+  c.nchunks = c.cinp / cc;
+  long long off = 0;
+  for (int cl = 0; cl < c.nclass; ++cl) {
+    c.kbc[cl] = fvc_rup(c.ntaps[cl] * (cc / 4), 2);
+    c.wcls[cl] = off;
+    off += (long long)c.nchunks * c.kbc[cl] * c.ntp * 128;
+  }
+  c.wtotal = off;
+  return true;
+}
+
+template <int CC, int WM, int WN>
+static int launch_t(const ConvArgs& a, dim3 grid, size_t lds, hipStream_t s) {
+  hipLaunchKernelGGL((conv_mfma_f32_kernel<CC, WM, WN>), grid, dim3(kThreads), lds, s, a);
+  FVC_CHECK_LAUNCH();
+  return 0;
+}
+
+template <int CC, int WM>
+static int launch_wn(int wn, const ConvArgs& a, dim3 grid, size_t lds, hipStream_t s) {
+  switch (wn) {
+    case 1: return launch_t<CC, WM, 1>(a, grid, lds, s);
+    case 2: return launch_t<CC, WM, 2>(a, grid, lds, s);
+    case 3: return launch_t<CC, WM, 3>(a, grid, lds, s);
+    case 4: return launch_t<CC, WM, 4>(a, grid, lds, s);
+  }
+  return FVC_EINVAL;
+}
+
+template <int CC>
+static int launch_wm(int wm, int wn, const ConvArgs& a, dim3 grid, size_t lds, hipStream_t s) {
+  if (wm == 1) return launch_wn<CC, 1>(wn, a, grid, lds, s);
+  return launch_wn<CC, 2>(wn, a, grid, lds, s);
+}
+
+static int run_conv(const float* x, const float* wpack, const float* bias, const float* res,
+                    float* y, int batch, int h, int w, int cin, int cout, int ks, int stride,
+                    int transposed, int in_op, int act, int post_op, hipStream_t s) {
+  Cfg c;
+  if (!make_cfg(cin, cout, ks, stride, transposed, c)) return FVC_EINVAL;
+  if (!x || !wpack || !bias || !y || batch <= 0 || h <= 0 || w <= 0) return FVC_EINVAL;
+  ConvArgs a;
+  a.x = x; a.w = wpack; a.bias = bias; a.res = res; a.y = y;
+  a.B = batch; a.H = h; a.W = w; a.cinp = c.cinp;
+  a.coutp = c.coutp; a.cout = cout;
+  if (!transposed) {
+    if (stride == 2 && ((h & 1) || (w & 1))) return FVC_EINVAL;
+    a.Ho = h / stride; a.Wo = w / stride;
+    a.Hq = a.Ho; a.Wq = a.Wo;
+  } else {
+    a.Ho = h * stride; a.Wo = w * stride;
+    a.Hq = h; a.Wq = w;
+  }
+  a.sin = c.sin; a.sout = c.sout; a.nclass = c.nclass; a.nchunks = c.nchunks; a.ntp = c.ntp;
+  a.dymin = c.dymin; a.dxmin = c.dxmin;
+  const int TH = 4 * c.wm;
+  a.ir = (TH - 1) * c.sin + 1 + (c.dymax - c.dymin);
+  a.ic = 31 * c.sin + 1 + (c.dxmax - c.dxmin);
+  a.in_op = in_op; a.act = act; a.post_op = post_op;
+  for (int cl = 0; cl < 4; ++cl) {
+    a.kbc[cl] = cl < c.nclass ? c.kbc[cl] : 0;
+    a.ntaps[cl] = cl < c.nclass ? c.ntaps[cl] : 0;
+    a.oy0[cl] = cl < c.nclass ? c.oy0[cl] : 0;
+    a.ox0[cl] = cl < c.nclass ? c.ox0[cl] : 0;
+    a.wcls[cl] = cl < c.nclass ? c.wcls[cl] : 0;
+    for (int t = 0; t < kMaxTaps; ++t) {
+      const bool v = cl < c.nclass && t < c.ntaps[cl];
+      a.tdy[cl][t] = (short)(v ? c.tdy[cl][t] : 0);
+      a.tdx[cl][t] = (short)(v ? c.tdx[cl][t] : 0);
+    }
+  }
+  const int cs = ((c.cc / 4) % 2 == 1) ? c.cc : c.cc + 4;
+  const size_t lds = 256 + (size_t)a.ir * a.ic * cs * 4;
+  const int tiles_x = fvc_cdiv(a.Wq, 32);
+  const int tiles_y = fvc_cdiv(a.Hq, TH);
+  dim3 grid(tiles_x * tiles_y, c.ntp / c.wn, batch * c.nclass);
+  switch (c.cc) {
+    case 4: return launch_wm<4>(c.wm, c.wn, a, grid, lds, s);
+    case 8: return launch_wm<8>(c.wm, c.wn, a, grid, lds, s);
+    case 16: return launch_wm<16>(c.wm, c.wn, a, grid, lds, s);
+    case 32: return launch_wm<32>(c.wm, c.wn, a, grid, lds, s);
+  }
+  return FVC_EINVAL;
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t fvc_conv_wpack_floats(int cin, int cout, int ksize, int stride, int transposed) {
+  Cfg c;
+  if (!make_cfg(cin, cout, ksize, stride, transposed, c)) return 0;
+  return (size_t)c.wtotal;
+}
+
+// w_host: conv OIHW [cout][cin][k][k]; deconv IOHW [cin][cout][k][k]
+int fvc_conv_pack_weight(const float* w, float* wp, int cin, int cout, int ks, int stride,
+                         int transposed) {
+  Cfg c;
+  if (!make_cfg(cin, cout, ks, stride, transposed, c) || !w || !wp) return FVC_EINVAL;
+  const int cc4 = c.cc / 4;
+  for (long long i = 0; i < c.wtotal; ++i) wp[i] = 0.f;
+  for (int cl = 0; cl < c.nclass; ++cl)
+    for (int ch = 0; ch < c.nchunks; ++ch)
+      for (int kb = 0; kb < c.ntaps[cl] * cc4; ++kb) {
+        const int t = kb / cc4, c4 = kb % cc4;
+        const int ky = c.tky[cl][t], kx = c.tkx[cl][t];
+        for (int j = 0; j < cout; ++j)
+          for (int e = 0; e < 4; ++e) {
+            const int ci = ch * c.cc + c4 * 4 + e;
+            if (ci >= cin) continue;
+            const float v = transposed ? w[(((size_t)ci * cout + j) * ks + ky) * ks + kx]
+                                       : w[(((size_t)j * cin + ci) * ks + ky) * ks + kx];
+            const size_t o = (size_t)c.wcls[cl] +
+                             (((size_t)ch * c.kbc[cl] + kb) * c.ntp * 32 + j) * 4 + e;
+            wp[o] = v;
+          }
+      }
+  return 0;
+}
+
+int fvc_conv2d_nhwc_f32(const float* x, const float* wpack, const float* bias, const float* res,
+                        float* y, int batch, int h, int w, int cin, int cout, int ksize,
+                        int stride, int in_op, int act, int post_op, fvc_stream_t stream) {
+  return run_conv(x, wpack, bias, res, y, batch, h, w, cin, cout, ksize, stride, 0, in_op, act,
+                  post_op, (hipStream_t)stream);
+}
+
+int fvc_deconv2d_nhwc_f32(const float* x, const float* wpack, const float* bias,
+                          const float* res, float* y, int batch, int h, int w, int cin, int cout,
+                          int ksize, int stride, int in_op, int act, int post_op,
+                          fvc_stream_t stream) {
+  return run_conv(x, wpack, bias, res, y, batch, h, w, cin, cout, ksize, stride, 1, in_op, act,
+                  post_op, (hipStream_t)stream);
+}
+
+}  // extern "C"

@@ -1,0 +1,549 @@
+// HBM-bound kernels of the DVC forward: layout conversion, pyramids, warp (grid_sample),
+// bilinear 2x upsampling, GDN, recon/loss finalisation and the bpp-estimate reductions.
+//
+// Float expressions that the reference computes as separate ATen ops are written with
+// contraction off (no FMA fusion) and in the reference's operand order, so results track the
+// CPU path to ~1 ulp.
+#include "fvc_common.h"
+#include <string.h>
+
+#pragma clang fp contract(off)
+
+namespace {
+
+constexpr int kBlk = 256;
+constexpr int kRedBlocks = 1024;  // fixed grid for deterministic reductions
+
+__device__ __forceinline__ int grid_stride_start() { return blockIdx.x * blockDim.x + threadIdx.x; }
+
+// ------------------------------------------------------------------ layout
+__global__ void k_nchw_to_nhwc(const float* __restrict__ src, float* __restrict__ dst, int B, int C,
+                               int H, int W, int cp) {
+  const size_t npix = (size_t)B * H * W;
+  for (size_t p = grid_stride_start(); p < npix; p += (size_t)gridDim.x * blockDim.x) {
+    const size_t b = p / ((size_t)H * W);
+    const size_t hw = p - b * H * W;
+    for (int c = 0; c < cp; ++c) {
+      dst[p * cp + c] = c < C ? src[(b * C + c) * H * W + hw] : 0.f;
+    }
+  }
+}
+
+__global__ void k_nhwc_to_nchw(const float* __restrict__ src, float* __restrict__ dst, int B, int C,
+                               int H, int W, int cp, int clamp01) {
+  const size_t n = (size_t)B * C * H * W;
+  for (size_t e = grid_stride_start(); e < n; e += (size_t)gridDim.x * blockDim.x) {
+    const size_t hw = e % ((size_t)H * W);
+    const size_t bc = e / ((size_t)H * W);
+    const size_t c = bc % C, b = bc / C;
+    const float v = src[(b * H * W + hw) * cp + c];
+    dst[e] = clamp01 ? fminf(fmaxf(v, 0.f), 1.f) : v;
+  }
+}
+
+// avg_pool2d(k=2,s=2): ((x00 + x01) + x10) + x11, then / 4 (ATen CPU order)
+__global__ void k_avgpool2(const float* __restrict__ src, float* __restrict__ dst, int B, int H, int W,
+                           int cp) {
+  const int Ho = H / 2, Wo = W / 2, c4n = cp / 4;
+  const size_t n = (size_t)B * Ho * Wo * c4n;
+  for (size_t e = grid_stride_start(); e < n; e += (size_t)gridDim.x * blockDim.x) {
+    const int c4 = e % c4n;
+    size_t p = e / c4n;
+    const int ox = p % Wo; p /= Wo;
+    const int oy = p % Ho;
+    const size_t b = p / Ho;
+    const float4* s = reinterpret_cast<const float4*>(src);
+    const size_t r0 = ((b * H + 2 * oy) * W + 2 * ox) * c4n + c4;
+    const size_t r1 = r0 + (size_t)W * c4n;
+    const float4 a = s[r0], bb = s[r0 + c4n], c = s[r1], d = s[r1 + c4n];
+    float4 o;
+    o.x = (((a.x + bb.x) + c.x) + d.x) / 4.f;
+    o.y = (((a.y + bb.y) + c.y) + d.y) / 4.f;
+    o.z = (((a.z + bb.z) + c.z) + d.z) / 4.f;
+    o.w = (((a.w + bb.w) + c.w) + d.w) / 4.f;
+    reinterpret_cast<float4*>(dst)[e] = o;
+  }
+}
+
+// ------------------------------------------------------------------ warp (torch_warp)
+// torch.linspace(-1, 1, n)[i] as ATen computes it (symmetric two-sided formula)
+__device__ __forceinline__ float linspace_m1p1(int i, int n) {
+  if (n == 1) return -1.f;
+  const float step = 2.f / (float)(n - 1);
+  const int half = n / 2;
+  return (i < half) ? (-1.f + step * (float)i) : (1.f - step * (float)(n - 1 - i));
+}
+
+struct WarpTap {
+  int x0, y0;
+  float nw, ne, sw, se;
+  bool vx1, vy1;
+};
+
+// grid = linspace grid + flow/((n-1)/2); grid_sample(bilinear, border, align_corners=False)
+// (endecoder.py:52-67; ATen CPU GridSamplerKernel unnormalize/clip/interp order)
+__device__ __forceinline__ WarpTap warp_tap(int y, int x, float fx, float fy, int H, int W) {
+  const float gx = linspace_m1p1(x, W) + fx / ((float)(W - 1) / 2.f);
+  const float gy = linspace_m1p1(y, H) + fy / ((float)(H - 1) / 2.f);
+  float ix = (gx + 1.f) * ((float)W / 2.f) - 0.5f;
+  float iy = (gy + 1.f) * ((float)H / 2.f) - 0.5f;
+  ix = fminf(fmaxf(ix, 0.f), (float)(W - 1));
+  iy = fminf(fmaxf(iy, 0.f), (float)(H - 1));
+  const float xw = floorf(ix), yn = floorf(iy);
+  const float w = ix - xw, e = 1.f - w;
+  const float n = iy - yn, s = 1.f - n;
+  WarpTap t;
+  t.x0 = (int)xw;
+  t.y0 = (int)yn;
+  t.nw = s * e; t.ne = s * w; t.sw = n * e; t.se = n * w;
+  t.vx1 = t.x0 + 1 < W;
+  t.vy1 = t.y0 + 1 < H;
+  return t;
+}
+
+__device__ __forceinline__ float4 warp_sample4(const float* im, size_t bbase, int W, int c4n, int c4,
+                                               const WarpTap& t) {
+  const float4* s = reinterpret_cast<const float4*>(im);
+  const size_t r0 = (bbase + (size_t)t.y0 * W + t.x0) * c4n + c4;
+  const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+  const float4 vnw = s[r0];
+  const float4 vne = t.vx1 ? s[r0 + c4n] : z;
+  const float4 vsw = t.vy1 ? s[r0 + (size_t)W * c4n] : z;
+  const float4 vse = (t.vx1 && t.vy1) ? s[r0 + (size_t)W * c4n + c4n] : z;
+  float4 o;
+  o.x = ((vnw.x * t.nw + vne.x * t.ne) + vsw.x * t.sw) + vse.x * t.se;
+  o.y = ((vnw.y * t.nw + vne.y * t.ne) + vsw.y * t.sw) + vse.y * t.se;
+  o.z = ((vnw.z * t.nw + vne.z * t.ne) + vsw.z * t.sw) + vse.z * t.se;
+  o.w = ((vnw.w * t.nw + vne.w * t.ne) + vsw.w * t.sw) + vse.w * t.se;
+  return o;
+}
+
+__global__ void k_warp(const float* __restrict__ im, const float* __restrict__ flow, float* __restrict__ out,
+                       int B, int H, int W, int cp) {
+  const int c4n = cp / 4;
+  const size_t npix = (size_t)B * H * W;
+  for (size_t p = grid_stride_start(); p < npix; p += (size_t)gridDim.x * blockDim.x) {
+    const int x = p % W;
+    const int y = (p / W) % H;
+    const size_t b = p / ((size_t)H * W);
+    const float4 f = reinterpret_cast<const float4*>(flow)[p];
+    const WarpTap t = warp_tap(y, x, f.x, f.y, H, W);
+    for (int c4 = 0; c4 < c4n; ++c4)
+      reinterpret_cast<float4*>(out)[p * c4n + c4] = warp_sample4(im, b * H * W, W, c4n, c4, t);
+  }
+}
+
+// ------------------------------------------------------------------ bilinear upsampling
+struct UpIdx {
+  int i0, i1;
+  float l0, l1;
+};
+
+// ATen compute_indices_weights_linear: src = ac ? scale*d : max(scale*(d+0.5)-0.5, 0)
+__device__ __forceinline__ UpIdx up_index(int d, int in, int out, int ac) {
+  float src;
+  if (ac) {
+    const float scale = out > 1 ? (float)(in - 1) / (float)(out - 1) : 0.f;
+    src = scale * (float)d;
+  } else {
+    const float scale = (float)in / (float)out;
+    src = fmaxf(scale * ((float)d + 0.5f) - 0.5f, 0.f);
+  }
+  int i0 = (int)floorf(src);
+  float lam = fminf(fmaxf(src - (float)i0, 0.f), 1.f);
+  if (i0 > in - 1) i0 = in - 1;
+  UpIdx u;
+  u.i0 = i0;
+  u.i1 = i0 + ((i0 < in - 1) ? 1 : 0);
+  u.l1 = lam;
+  u.l0 = 1.f - lam;
+  return u;
+}
+
+__device__ __forceinline__ float4 up_sample4(const float* src, size_t bbase, int w, int c4n, int c4,
+                                             const UpIdx& uy, const UpIdx& ux) {
+  const float4* s = reinterpret_cast<const float4*>(src);
+  const float4 a = s[(bbase + (size_t)uy.i0 * w + ux.i0) * c4n + c4];
+  const float4 b = s[(bbase + (size_t)uy.i0 * w + ux.i1) * c4n + c4];
+  const float4 c = s[(bbase + (size_t)uy.i1 * w + ux.i0) * c4n + c4];
+  const float4 d = s[(bbase + (size_t)uy.i1 * w + ux.i1) * c4n + c4];
+  float4 o;
+  o.x = (a.x * ux.l0 + b.x * ux.l1) * uy.l0 + (c.x * ux.l0 + d.x * ux.l1) * uy.l1;
+  o.y = (a.y * ux.l0 + b.y * ux.l1) * uy.l0 + (c.y * ux.l0 + d.y * ux.l1) * uy.l1;
+  o.z = (a.z * ux.l0 + b.z * ux.l1) * uy.l0 + (c.z * ux.l0 + d.z * ux.l1) * uy.l1;
+  o.w = (a.w * ux.l0 + b.w * ux.l1) * uy.l0 + (c.w * ux.l0 + d.w * ux.l1) * uy.l1;
+  return o;
+}
+
+__global__ void k_up2_add(const float* __restrict__ src, const float* __restrict__ skip, float* __restrict__ out,
+                          int B, int h, int w, int cp, int ac, float scale) {
+  const int H = 2 * h, W = 2 * w, c4n = cp / 4;
+  const size_t n = (size_t)B * H * W * c4n;
+  for (size_t e = grid_stride_start(); e < n; e += (size_t)gridDim.x * blockDim.x) {
+    const int c4 = e % c4n;
+    size_t p = e / c4n;
+    const int x = p % W; p /= W;
+    const int y = p % H;
+    const size_t b = p / H;
+    const UpIdx uy = up_index(y, h, H, ac), ux = up_index(x, w, W, ac);
+    float4 v = up_sample4(src, b * h * w, w, c4n, c4, uy, ux);
+    if (scale != 1.f) { v.x *= scale; v.y *= scale; v.z *= scale; v.w *= scale; }
+    if (skip) {
+      const float4 s = reinterpret_cast<const float4*>(skip)[e];
+      v.x = s.x + v.x; v.y = s.y + v.y; v.z = s.z + v.z; v.w = s.w + v.w;
+    }
+    reinterpret_cast<float4*>(out)[e] = v;
+  }
+}
+
+// ------------------------------------------------------------------ SpyNet level assembly
+__global__ void k_spynet_assemble(const float* __restrict__ im1, const float* __restrict__ im2,
+                                  const float* __restrict__ flow_prev, float* __restrict__ flow_up,
+                                  float* __restrict__ x8, int B, int H, int W) {
+  const size_t npix = (size_t)B * H * W;
+  const int h = H / 2, w = W / 2;
+  for (size_t p = grid_stride_start(); p < npix; p += (size_t)gridDim.x * blockDim.x) {
+    const int x = p % W;
+    const int y = (p / W) % H;
+    const size_t b = p / ((size_t)H * W);
+    float4 fu = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (flow_prev) {
+      const UpIdx uy = up_index(y, h, H, 0), ux = up_index(x, w, W, 0);
+      fu = up_sample4(flow_prev, b * h * w, w, 1, 0, uy, ux);
+      fu.x = fu.x * 2.f; fu.y = fu.y * 2.f; fu.z = 0.f; fu.w = 0.f;
+    }
+    reinterpret_cast<float4*>(flow_up)[p] = fu;
+    const WarpTap t = warp_tap(y, x, fu.x, fu.y, H, W);
+    const float4 wv = warp_sample4(im2, b * H * W, W, 1, 0, t);
+    const float4 a = reinterpret_cast<const float4*>(im1)[p];
+    float4* o = reinterpret_cast<float4*>(x8) + p * 2;
+    o[0] = make_float4(a.x, a.y, a.z, wv.x);
+    o[1] = make_float4(wv.y, wv.z, fu.x, fu.y);
+  }
+}
+
+// motion compensation input: warpframe = warp(ref, mv); x8 = [warpframe, ref, 0, 0]
+__global__ void k_mc_assemble(const float* __restrict__ ref, const float* __restrict__ mv,
+                              float* __restrict__ warpframe, float* __restrict__ x8, int B, int H, int W) {
+  const size_t npix = (size_t)B * H * W;
+  for (size_t p = grid_stride_start(); p < npix; p += (size_t)gridDim.x * blockDim.x) {
+    const int x = p % W;
+    const int y = (p / W) % H;
+    const size_t b = p / ((size_t)H * W);
+    const float4 f = reinterpret_cast<const float4*>(mv)[p];
+    const WarpTap t = warp_tap(y, x, f.x, f.y, H, W);
+    float4 wv = warp_sample4(ref, b * H * W, W, 1, 0, t);
+    wv.w = 0.f;
+    reinterpret_cast<float4*>(warpframe)[p] = wv;
+    const float4 r = reinterpret_cast<const float4*>(ref)[p];
+    float4* o = reinterpret_cast<float4*>(x8) + p * 2;
+    o[0] = make_float4(wv.x, wv.y, wv.z, r.x);
+    o[1] = make_float4(r.y, r.z, 0.f, 0.f);
+  }
+}
+
+__global__ void k_sub(const float* __restrict__ a, const float* __restrict__ b, float* __restrict__ o, size_t n) {
+  for (size_t e = grid_stride_start(); e < n; e += (size_t)gridDim.x * blockDim.x) o[e] = a[e] - b[e];
+}
+
+// ------------------------------------------------------------------ GDN / IGDN (C = 64)
+// norm_i = beta_i + sum_j gamma[i][j] x_j^2 ; y = x / sqrt(norm) (or x * sqrt(norm))
+template <int C>
+__global__ __launch_bounds__(kBlk) void k_gdn(const float* __restrict__ x, float* __restrict__ y,
+                                              const float* __restrict__ beta, const float* __restrict__ gamma,
+                                              size_t npix, int inverse) {
+  __shared__ float sg[C * C];
+  __shared__ float sb[C];
+  for (int i = threadIdx.x; i < C * C; i += blockDim.x) sg[i] = gamma[i];
+  for (int i = threadIdx.x; i < C; i += blockDim.x) sb[i] = beta[i];
+  __syncthreads();
+  for (size_t p = grid_stride_start(); p < npix; p += (size_t)gridDim.x * blockDim.x) {
+    float xv[C], x2[C];
+    const float4* xs = reinterpret_cast<const float4*>(x + p * C);
+#pragma unroll
+    for (int k = 0; k < C / 4; ++k) {
+      const float4 v = xs[k];
+      xv[4 * k] = v.x; xv[4 * k + 1] = v.y; xv[4 * k + 2] = v.z; xv[4 * k + 3] = v.w;
+    }
+#pragma unroll
+    for (int j = 0; j < C; ++j) x2[j] = xv[j] * xv[j];
+    float4* ys = reinterpret_cast<float4*>(y + p * C);
+#pragma unroll
+    for (int k = 0; k < C / 4; ++k) {
+      float o[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int i = 4 * k + u;
+        float acc = sb[i];
+#pragma unroll
+        for (int j = 0; j < C; ++j) acc = __builtin_fmaf(sg[i * C + j], x2[j], acc);
+        const float nrm = sqrtf(acc);
+        o[u] = inverse ? xv[i] * nrm : xv[i] / nrm;
+      }
+      ys[k] = make_float4(o[0], o[1], o[2], o[3]);
+    }
+  }
+}
+
+// ------------------------------------------------------------------ deterministic reductions
+template <int K>
+__device__ void block_reduce_store(double (&v)[K], double* out) {
+  __shared__ double red[kBlk / 64][K];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    double s = v[k];
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_down(s, off, 64);
+    if (lane == 0) red[wid][k] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      double s = 0.0;
+      for (int w = 0; w < kBlk / 64; ++w) s += red[w][k];
+      out[blockIdx.x * K + k] = s;
+    }
+  }
+}
+
+template <int K>
+__global__ void k_reduce_partials(const double* __restrict__ ws, int nblocks, double* __restrict__ out) {
+  __shared__ double red[kBlk][K];
+  double s[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) s[k] = 0.0;
+  for (int i = threadIdx.x; i < nblocks; i += blockDim.x)
+#pragma unroll
+    for (int k = 0; k < K; ++k) s[k] += ws[i * K + k];
+#pragma unroll
+  for (int k = 0; k < K; ++k) red[threadIdx.x][k] = s[k];
+  __syncthreads();
+  for (int st = kBlk / 2; st > 0; st >>= 1) {
+    if (threadIdx.x < st)
+#pragma unroll
+      for (int k = 0; k < K; ++k) red[threadIdx.x][k] += red[threadIdx.x + st][k];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0)
+#pragma unroll
+    for (int k = 0; k < K; ++k) out[k] = red[0][k];
+}
+
+__global__ __launch_bounds__(kBlk) void k_recon_finalize(const float* __restrict__ recon, const float* __restrict__ in,
+                                                         const float* __restrict__ wf, const float* __restrict__ pred,
+                                                         float* __restrict__ clipped, double* __restrict__ ws,
+                                                         int B, int H, int W) {
+  double acc[3] = {0.0, 0.0, 0.0};
+  const size_t npix = (size_t)B * H * W;
+  const size_t hw = (size_t)H * W;
+  for (size_t p = grid_stride_start(); p < npix; p += (size_t)gridDim.x * blockDim.x) {
+    const float4 r = reinterpret_cast<const float4*>(recon)[p];
+    const float4 x = reinterpret_cast<const float4*>(in)[p];
+    const float4 wv = reinterpret_cast<const float4*>(wf)[p];
+    const float4 pv = reinterpret_cast<const float4*>(pred)[p];
+    const float rr[3] = {r.x, r.y, r.z}, xx[3] = {x.x, x.y, x.z};
+    const float ww[3] = {wv.x, wv.y, wv.z}, pp[3] = {pv.x, pv.y, pv.z};
+    const size_t b = p / hw, q = p - b * hw;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const float d0 = rr[c] - xx[c], d1 = ww[c] - xx[c], d2 = pp[c] - xx[c];
+      acc[0] += (double)(d0 * d0);
+      acc[1] += (double)(d1 * d1);
+      acc[2] += (double)(d2 * d2);
+      clipped[(b * 3 + c) * hw + q] = fminf(fmaxf(rr[c], 0.f), 1.f);
+    }
+  }
+  block_reduce_store<3>(acc, ws);
+}
+
+// Laplace bits (net.py:121-151): p = cdf(f+.5) - cdf(f-.5), cdf(v) = .5 - .5 sign(v) expm1(-|v|/s)
+__device__ __forceinline__ float laplace_cdf(float v, float s) {
+  const float sg = v > 0.f ? 1.f : (v < 0.f ? -1.f : 0.f);
+  return 0.5f - 0.5f * sg * expm1f(-fabsf(v) / s);
+}
+
+__device__ __forceinline__ float bits_of_prob(float p) {
+  float b = -1.0f * logf(p + 1e-5f) / 0.6931471805599453f;
+  return fminf(fmaxf(b, 0.f), 50.f);
+}
+
+__global__ __launch_bounds__(kBlk) void k_bits_laplace(const float* __restrict__ feat, const float* __restrict__ sigma,
+                                                       double* __restrict__ ws, size_t npix, int C, int cp) {
+  double acc[1] = {0.0};
+  const size_t n = npix * C;
+  for (size_t e = grid_stride_start(); e < n; e += (size_t)gridDim.x * blockDim.x) {
+    const size_t p = e / C;
+    const int c = e - p * C;
+    const float f = rintf(feat[p * cp + c]);
+    const float s = fminf(fmaxf(sigma[p * cp + c], 1e-5f), 1e10f);
+    const float prob = laplace_cdf(f + 0.5f, s) - laplace_cdf(f - 0.5f, s);
+    acc[0] += (double)bits_of_prob(prob);
+  }
+  block_reduce_store<1>(acc, ws);
+}
+
+__device__ __forceinline__ float softplus_f(float v) { return v > 20.f ? v : log1pf(expf(v)); }
+
+__device__ __forceinline__ float bitest_cdf(float x, const float* prm, int C, int c) {
+#pragma unroll
+  for (int f = 0; f < 3; ++f) {
+    const float h = prm[(3 * f) * C + c], b = prm[(3 * f + 1) * C + c], a = prm[(3 * f + 2) * C + c];
+    x = x * softplus_f(h) + b;
+    x = x + tanhf(x) * tanhf(a);
+  }
+  const float h = prm[9 * C + c], b = prm[10 * C + c];
+  const float t = x * softplus_f(h) + b;
+  return 1.f / (1.f + expf(-t));
+}
+
+__global__ __launch_bounds__(kBlk) void k_bits_factorized(const float* __restrict__ v, const float* __restrict__ prm,
+                                                          double* __restrict__ ws, size_t npix, int C, int cp) {
+  double acc[1] = {0.0};
+  const size_t n = npix * C;
+  for (size_t e = grid_stride_start(); e < n; e += (size_t)gridDim.x * blockDim.x) {
+    const size_t p = e / C;
+    const int c = e - p * C;
+    const float q = rintf(v[p * cp + c]);
+    const float prob = bitest_cdf(q + 0.5f, prm, C, c) - bitest_cdf(q - 0.5f, prm, C, c);
+    acc[0] += (double)bits_of_prob(prob);
+  }
+  block_reduce_store<1>(acc, ws);
+}
+
+static int grid_for(size_t n) {
+  size_t g = (n + kBlk - 1) / kBlk;
+  if (g > 8192) g = 8192;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+}  // namespace
+
+extern "C" {
+
+int fvc_version(void) { return 1; }
+
+int fvc_device_arch_ok(void) {
+  hipDeviceProp_t p;
+  if (hipGetDeviceProperties(&p, 0) != hipSuccess) return 0;
+  return strncmp(p.gcnArchName, "gfx950", 6) == 0 ? 1 : 0;
+}
+
+int fvc_nchw_to_nhwc(const float* src, float* dst, int batch, int c, int h, int w, int cp, fvc_stream_t s) {
+  if (!src || !dst || c > cp || cp % 4) return FVC_EINVAL;
+  const size_t n = (size_t)batch * h * w;
+  hipLaunchKernelGGL(k_nchw_to_nhwc, dim3(grid_for(n)), dim3(kBlk), 0, (hipStream_t)s, src, dst, batch, c, h, w, cp);
+  FVC_CHECK_LAUNCH();
+  return 0;
+}
+
+int fvc_nhwc_to_nchw(const float* src, float* dst, int batch, int c, int h, int w, int cp, int clamp01,
+                     fvc_stream_t s) {
+  if (!src || !dst || c > cp) return FVC_EINVAL;
+  const size_t n = (size_t)batch * c * h * w;
+  hipLaunchKernelGGL(k_nhwc_to_nchw, dim3(grid_for(n)), dim3(kBlk), 0, (hipStream_t)s, src, dst, batch, c, h, w, cp,
+                     clamp01);
+  FVC_CHECK_LAUNCH();
+  return 0;
+}
+
+int fvc_avgpool2_nhwc(const float* src, float* dst, int batch, int h, int w, int cp, fvc_stream_t s) {
+  if (!src || !dst || (h & 1) || (w & 1) || cp % 4) return FVC_EINVAL;
+  const size_t n = (size_t)batch * (h / 2) * (w / 2) * (cp / 4);
+  hipLaunchKernelGGL(k_avgpool2, dim3(grid_for(n)), dim3(kBlk), 0, (hipStream_t)s, src, dst, batch, h, w, cp);
+  FVC_CHECK_LAUNCH();
+  return 0;
+}
+
+int fvc_warp_nhwc(const float* im, const float* flow, float* out, int batch, int h, int w, int cp, fvc_stream_t s) {
+  if (!im || !flow || !out || cp % 4 || h < 2 || w < 2) return FVC_EINVAL;
+  const size_t n = (size_t)batch * h * w;
+  hipLaunchKernelGGL(k_warp, dim3(grid_for(n)), dim3(kBlk), 0, (hipStream_t)s, im, flow, out, batch, h, w, cp);
+  FVC_CHECK_LAUNCH();
+  return 0;
+}
+
+int fvc_upsample2x_add_nhwc(const float* src, const float* skip, float* out, int batch, int h, int w, int cp,
+                            int align_corners, float scale, fvc_stream_t s) {
+  if (!src || !out || cp % 4) return FVC_EINVAL;
+  const size_t n = (size_t)batch * 4 * h * w * (cp / 4);
+  hipLaunchKernelGGL(k_up2_add, dim3(grid_for(n)), dim3(kBlk), 0, (hipStream_t)s, src, skip, out, batch, h, w, cp,
+                     align_corners, scale);
+  FVC_CHECK_LAUNCH();
+  return 0;
+}
+
+int fvc_spynet_assemble(const float* im1, const float* im2, const float* flow_prev, float* flow_up, float* x8,
+                        int batch, int h, int w, fvc_stream_t s) {
+  if (!im1 || !im2 || !flow_up || !x8 || (h & 1) || (w & 1) || h < 2 || w < 2) return FVC_EINVAL;
+  const size_t n = (size_t)batch * h * w;
+  hipLaunchKernelGGL(k_spynet_assemble, dim3(grid_for(n)), dim3(kBlk), 0, (hipStream_t)s, im1, im2, flow_prev,
+                     flow_up, x8, batch, h, w);
+  FVC_CHECK_LAUNCH();
+  return 0;
+}
+
+int fvc_mc_assemble(const float* ref, const float* mv, float* warpframe, float* x8, int batch, int h, int w,
+                    fvc_stream_t s) {
+  if (!ref || !mv || !warpframe || !x8 || h < 2 || w < 2) return FVC_EINVAL;
+  const size_t n = (size_t)batch * h * w;
+  hipLaunchKernelGGL(k_mc_assemble, dim3(grid_for(n)), dim3(kBlk), 0, (hipStream_t)s, ref, mv, warpframe, x8,
+                     batch, h, w);
+  FVC_CHECK_LAUNCH();
+  return 0;
+}
+
+int fvc_sub_f32(const float* a, const float* b, float* out, size_t n, fvc_stream_t s) {
+  if (!a || !b || !out) return FVC_EINVAL;
+  hipLaunchKernelGGL(k_sub, dim3(grid_for(n)), dim3(kBlk), 0, (hipStream_t)s, a, b, out, n);
+  FVC_CHECK_LAUNCH();
+  return 0;
+}
+
+int fvc_gdn_nhwc(const float* x, float* y, const float* beta, const float* gamma, int batch, int h, int w, int c,
+                 int inverse, fvc_stream_t s) {
+  if (!x || !y || !beta || !gamma || c != 64) return FVC_EINVAL;
+  const size_t npix = (size_t)batch * h * w;
+  hipLaunchKernelGGL(k_gdn<64>, dim3(grid_for(npix)), dim3(kBlk), 0, (hipStream_t)s, x, y, beta, gamma, npix,
+                     inverse);
+  FVC_CHECK_LAUNCH();
+  return 0;
+}
+
+size_t fvc_reduce_ws_doubles(void) { return (size_t)kRedBlocks * 4; }
+
+int fvc_recon_finalize(const float* recon, const float* input, const float* warpframe, const float* prediction,
+                       float* clipped, double* out3, double* ws, int batch, int h, int w, fvc_stream_t s) {
+  if (!recon || !input || !warpframe || !prediction || !clipped || !out3 || !ws) return FVC_EINVAL;
+  hipLaunchKernelGGL(k_recon_finalize, dim3(kRedBlocks), dim3(kBlk), 0, (hipStream_t)s, recon, input, warpframe,
+                     prediction, clipped, ws, batch, h, w);
+  FVC_CHECK_LAUNCH();
+  hipLaunchKernelGGL(k_reduce_partials<3>, dim3(1), dim3(kBlk), 0, (hipStream_t)s, ws, kRedBlocks, out3);
+  FVC_CHECK_LAUNCH();
+  return 0;
+}
+
+int fvc_bits_laplace(const float* feature, const float* sigma, double* out1, double* ws, int batch, int h, int w,
+                     int c, int cp, fvc_stream_t s) {
+  if (!feature || !sigma || !out1 || !ws || c > cp) return FVC_EINVAL;
+  hipLaunchKernelGGL(k_bits_laplace, dim3(kRedBlocks), dim3(kBlk), 0, (hipStream_t)s, feature, sigma, ws,
+                     (size_t)batch * h * w, c, cp);
+  FVC_CHECK_LAUNCH();
+  hipLaunchKernelGGL(k_reduce_partials<1>, dim3(1), dim3(kBlk), 0, (hipStream_t)s, ws, kRedBlocks, out1);
+  FVC_CHECK_LAUNCH();
+  return 0;
+}
+
+int fvc_bits_factorized(const float* v, const float* params, double* out1, double* ws, int batch, int h, int w,
+                        int c, int cp, fvc_stream_t s) {
+  if (!v || !params || !out1 || !ws || c > cp) return FVC_EINVAL;
+  hipLaunchKernelGGL(k_bits_factorized, dim3(kRedBlocks), dim3(kBlk), 0, (hipStream_t)s, v, params, ws,
+                     (size_t)batch * h * w, c, cp);
+  FVC_CHECK_LAUNCH();
+  hipLaunchKernelGGL(k_reduce_partials<1>, dim3(1), dim3(kBlk), 0, (hipStream_t)s, ws, kRedBlocks, out1);
+  FVC_CHECK_LAUNCH();
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,260 @@
+"""Typed wrappers over the libfvc C-ABI for torch device tensors.
+
+Tensors are passed by raw device pointer (``data_ptr``) together with their sizes and the
+current HIP stream; every wrapper checks shapes/dtypes/contiguity before launching, since the
+kernels trust their arguments (an out-of-bounds launch can fault the whole GPU).
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib, profiling
+
+IN_NONE, IN_RELU, IN_ABS, IN_ROUND = 0, 1, 2, 3
+ACT_NONE, ACT_RELU, ACT_LRELU = 0, 1, 2
+POST_NONE, POST_EXP = 0, 1
+
+
+def cp4(c: int) -> int:
+    return (c + 3) // 4 * 4
+
+
+def stream_handle(device=None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def _ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+def _chk(t, shape=None, dtype=torch.float32, name="tensor"):
+    if t is None:
+        return
+    if not t.is_cuda:
+        raise ValueError(f"{name}: libfvc kernels need a device tensor (got {t.device})")
+    if t.dtype != dtype:
+        raise ValueError(f"{name}: expected {dtype}, got {t.dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name}: must be contiguous")
+    if shape is not None and tuple(t.shape) != tuple(shape):
+        raise ValueError(f"{name}: expected shape {tuple(shape)}, got {tuple(t.shape)}")
+
+
+def empty_nhwc(b, h, w, c, like):
+    return torch.empty((b, h, w, cp4(c)), dtype=torch.float32, device=like.device)
+
+
+# ------------------------------------------------------------------ layout
+def nchw_to_nhwc(x: torch.Tensor, cp: int | None = None) -> torch.Tensor:
+    B, C, H, W = x.shape
+    cp = cp or cp4(C)
+    _chk(x, name="x")
+    y = torch.empty((B, H, W, cp), dtype=torch.float32, device=x.device)
+    _lib.call("fvc_nchw_to_nhwc", x.data_ptr(), y.data_ptr(), B, C, H, W, cp, stream_handle())
+    return y
+
+
+def nhwc_to_nchw(x: torch.Tensor, c: int, clamp01: bool = False) -> torch.Tensor:
+    B, H, W, cp = x.shape
+    _chk(x, name="x")
+    y = torch.empty((B, c, H, W), dtype=torch.float32, device=x.device)
+    _lib.call("fvc_nhwc_to_nchw", x.data_ptr(), y.data_ptr(), B, c, H, W, cp, int(clamp01), stream_handle())
+    return y
+
+
+def avgpool2(x: torch.Tensor) -> torch.Tensor:
+    B, H, W, cp = x.shape
+    _chk(x, name="x")
+    y = torch.empty((B, H // 2, W // 2, cp), dtype=torch.float32, device=x.device)
+    _lib.call("fvc_avgpool2_nhwc", x.data_ptr(), y.data_ptr(), B, H, W, cp, stream_handle())
+    return y
+
+
+def warp(im: torch.Tensor, flow: torch.Tensor) -> torch.Tensor:
+    B, H, W, cp = im.shape
+    _chk(im, name="im")
+    _chk(flow, (B, H, W, 4), name="flow")
+    y = torch.empty_like(im)
+    _lib.call("fvc_warp_nhwc", im.data_ptr(), flow.data_ptr(), y.data_ptr(), B, H, W, cp, stream_handle())
+    return y
+
+
+def upsample2x_add(src, skip=None, align_corners=True, scale=1.0):
+    B, h, w, cp = src.shape
+    _chk(src, name="src")
+    _chk(skip, (B, 2 * h, 2 * w, cp), name="skip")
+    y = torch.empty((B, 2 * h, 2 * w, cp), dtype=torch.float32, device=src.device)
+    _lib.call("fvc_upsample2x_add_nhwc", src.data_ptr(), _ptr(skip), y.data_ptr(), B, h, w, cp,
+              int(align_corners), float(scale), stream_handle())
+    return y
+
+
+def spynet_assemble(im1, im2, flow_prev):
+    B, H, W, _ = im1.shape
+    _chk(im1, (B, H, W, 4), name="im1")
+    _chk(im2, (B, H, W, 4), name="im2")
+    _chk(flow_prev, (B, H // 2, W // 2, 4), name="flow_prev")
+    flow_up = torch.empty((B, H, W, 4), dtype=torch.float32, device=im1.device)
+    x8 = torch.empty((B, H, W, 8), dtype=torch.float32, device=im1.device)
+    _lib.call("fvc_spynet_assemble", im1.data_ptr(), im2.data_ptr(), _ptr(flow_prev), flow_up.data_ptr(),
+              x8.data_ptr(), B, H, W, stream_handle())
+    return flow_up, x8
+
+
+def mc_assemble(ref, mv):
+    B, H, W, _ = ref.shape
+    _chk(ref, (B, H, W, 4), name="ref")
+    _chk(mv, (B, H, W, 4), name="mv")
+    warpframe = torch.empty((B, H, W, 4), dtype=torch.float32, device=ref.device)
+    x8 = torch.empty((B, H, W, 8), dtype=torch.float32, device=ref.device)
+    _lib.call("fvc_mc_assemble", ref.data_ptr(), mv.data_ptr(), warpframe.data_ptr(), x8.data_ptr(), B, H, W,
+              stream_handle())
+    return warpframe, x8
+
+
+def sub(a, b):
+    _chk(a, name="a")
+    _chk(b, a.shape, name="b")
+    y = torch.empty_like(a)
+    _lib.call("fvc_sub_f32", a.data_ptr(), b.data_ptr(), y.data_ptr(), a.numel(), stream_handle())
+    return y
+
+
+def gdn(x, beta, gamma, inverse):
+    B, H, W, C = x.shape
+    _chk(x, name="x")
+    _chk(beta, (C,), name="beta")
+    _chk(gamma, (C, C), name="gamma")
+    y = torch.empty_like(x)
+    _lib.call("fvc_gdn_nhwc", x.data_ptr(), y.data_ptr(), beta.data_ptr(), gamma.data_ptr(), B, H, W, C,
+              int(inverse), stream_handle())
+    return y
+
+
+# ------------------------------------------------------------------ conv
+class PackedConv:
+    """A conv / transposed conv with weights packed for the MFMA kernel."""
+
+    def __init__(self, weight: torch.Tensor, bias: torch.Tensor, ksize: int, stride: int, transposed: bool,
+                 device):
+        lib = _lib.load()
+        w = weight.detach().to("cpu", torch.float32).contiguous()
+        if transposed:
+            cin, cout = w.shape[0], w.shape[1]
+        else:
+            cout, cin = w.shape[0], w.shape[1]
+        n = lib.fvc_conv_wpack_floats(cin, cout, ksize, stride, int(transposed))
+        if n == 0:
+            raise ValueError(f"unsupported conv geometry cin={cin} cout={cout} k={ksize} s={stride}")
+        packed = torch.empty(n, dtype=torch.float32)
+        _lib.call("fvc_conv_pack_weight", w.data_ptr(), packed.data_ptr(), cin, cout, ksize, stride,
+                  int(transposed))
+        self.wpack = packed.to(device)
+        self.bias = bias.detach().to(device, torch.float32).contiguous()
+        self.cin, self.cout, self.ksize, self.stride, self.transposed = cin, cout, ksize, stride, transposed
+
+    def out_hw(self, h, w):
+        if self.transposed:
+            return h * self.stride, w * self.stride
+        return h // self.stride, w // self.stride
+
+    def __call__(self, x, in_op=IN_NONE, act=ACT_NONE, post=POST_NONE, res=None, out=None):
+        B, H, W, cp = x.shape
+        if cp != cp4(self.cin):
+            raise ValueError(f"conv input has {cp} channels, expected {cp4(self.cin)}")
+        if (not self.transposed) and self.stride == 2 and (H % 2 or W % 2):
+            raise ValueError("stride-2 conv needs even input size")
+        _chk(x, name="x")
+        ho, wo = self.out_hw(H, W)
+        oshape = (B, ho, wo, cp4(self.cout))
+        _chk(res, oshape, name="res")
+        y = out if out is not None else torch.empty(oshape, dtype=torch.float32, device=x.device)
+        _chk(y, oshape, name="y")
+        fn = "fvc_deconv2d_nhwc_f32" if self.transposed else "fvc_conv2d_nhwc_f32"
+        timer = profiling.active()
+        if timer is not None:
+            ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            ev0.record()
+        _lib.call(fn, x.data_ptr(), self.wpack.data_ptr(), self.bias.data_ptr(), _ptr(res), y.data_ptr(), B, H, W,
+                  self.cin, self.cout, self.ksize, self.stride, in_op, act, post, stream_handle())
+        if timer is not None:
+            ev1.record()
+            timer.records.append((ev0, ev1, profiling.conv_flops(self.cin, self.cout, self.ksize, self.stride,
+                                                                 self.transposed, B, H, W)))
+        return y
+
+
+# ------------------------------------------------------------------ reductions
+_WS = {}
+
+
+def _ws(device):
+    key = str(device)
+    if key not in _WS:
+        n = _lib.load().fvc_reduce_ws_doubles()
+        _WS[key] = torch.empty(n, dtype=torch.float64, device=device)
+    return _WS[key]
+
+
+def recon_finalize(recon, inp, warpframe, prediction):
+    B, H, W, _ = recon.shape
+    for t, n in ((recon, "recon"), (inp, "input"), (warpframe, "warpframe"), (prediction, "prediction")):
+        _chk(t, (B, H, W, 4), name=n)
+    clipped = torch.empty((B, 3, H, W), dtype=torch.float32, device=recon.device)
+    out3 = torch.empty(3, dtype=torch.float64, device=recon.device)
+    _lib.call("fvc_recon_finalize", recon.data_ptr(), inp.data_ptr(), warpframe.data_ptr(), prediction.data_ptr(),
+              clipped.data_ptr(), out3.data_ptr(), _ws(recon.device).data_ptr(), B, H, W, stream_handle())
+    return clipped, out3
+
+
+def bits_laplace(feature, sigma, c):
+    B, H, W, cp = feature.shape
+    _chk(feature, name="feature")
+    _chk(sigma, feature.shape, name="sigma")
+    out = torch.empty(1, dtype=torch.float64, device=feature.device)
+    _lib.call("fvc_bits_laplace", feature.data_ptr(), sigma.data_ptr(), out.data_ptr(),
+              _ws(feature.device).data_ptr(), B, H, W, c, cp, stream_handle())
+    return out
+
+
+def bits_factorized(v, params, c):
+    B, H, W, cp = v.shape
+    _chk(v, name="v")
+    _chk(params, (11, c), name="params")
+    out = torch.empty(1, dtype=torch.float64, device=v.device)
+    _lib.call("fvc_bits_factorized", v.data_ptr(), params.data_ptr(), out.data_ptr(), _ws(v.device).data_ptr(),
+              B, H, W, c, cp, stream_handle())
+    return out
+
+
+# ------------------------------------------------------------------ entropy coding
+def latent_to_symbols(lat, c):
+    B, H, W, cp = lat.shape
+    _chk(lat, name="latent")
+    sym = torch.empty((B, c, H * W), dtype=torch.int32, device=lat.device)
+    _lib.call("fvc_latent_to_symbols", lat.data_ptr(), sym.data_ptr(), B, H, W, c, cp, stream_handle())
+    return sym
+
+
+def symbols_to_latent(sym, h, w, c):
+    B = sym.shape[0]
+    _chk(sym, (B, c, h * w), dtype=torch.int32, name="symbols")
+    lat = torch.empty((B, h, w, cp4(c)), dtype=torch.float32, device=sym.device)
+    _lib.call("fvc_symbols_to_latent", sym.data_ptr(), lat.data_ptr(), B, h, w, c, cp4(c), stream_handle())
+    return lat
+
+
+def build_indexes(sigma, scale_table, c):
+    B, H, W, cp = sigma.shape
+    _chk(sigma, name="sigma")
+    _chk(scale_table, name="scale_table")
+    idx = torch.empty((B, c, H * W), dtype=torch.int32, device=sigma.device)
+    _lib.call("fvc_build_indexes", sigma.data_ptr(), scale_table.data_ptr(), scale_table.numel(), idx.data_ptr(),
+              B, H, W, c, cp, stream_handle())
+    return idx
+
+
+def channel_indexes(b, hw, c, device):
+    idx = torch.empty((b, c, hw), dtype=torch.int32, device=device)
+    _lib.call("fvc_channel_indexes", idx.data_ptr(), b, hw, c, stream_handle())
+    return idx

@@ -1,0 +1,132 @@
+"""Drop-in mirror of the reference ``models.py`` surface for the DVC-pretrained path.
+
+``get_codec_model('DVC-pretrained', ...)`` (models.py:32-36 -> get_DVC_pretrained 1432-1445)
+returns a ``VideoCompressor`` carrying the attributes the reference GOP driver reads
+(``name``, ``compression_level``, ``loss_type``, ``I_level``, ``r``). ``parallel_compression``
+(models.py:233-410, DVC-pretrained branch 368-383) and ``PSNR`` (460-473) keep the reference
+signatures and return values, so ``eval.py``'s ``static_simulation_model`` can call them
+unchanged.
+
+The I-frame codec (BPG via ``os.system``, models.py:412-429) is out of scope: ``I_compression``
+passes the I-frame through losslessly and reports bpp 0 / PSNR inf (documented in DESIGN.md).
+"""
+from __future__ import annotations
+
+import math
+import os
+
+import torch
+
+from .net import VideoCompressor
+from .weights import seeded_torch_state_dict
+
+_RATIO_LIST = [256, 512, 1024, 2048, 2048 * 2, 2048 * 4, 2048 * 8]
+_I_LVL_LIST = [37, 32, 27, 22, 17, 12, 7]
+
+
+def get_DVC_pretrained(level, checkpoint=None, seed=20261015, device=None):
+    """models.py:1432-1445. The reference loads DVC/snapshot/{r}.model (absent offline); here a
+    checkpoint path may be given, otherwise the build's seeded weights are used."""
+    model = VideoCompressor()
+    model.name = "DVC-pretrained"
+    model.compression_level = level
+    model.loss_type = "P"
+    model.I_level = _I_LVL_LIST[level]
+    model.r = _RATIO_LIST[level]
+    if checkpoint is not None and os.path.isfile(checkpoint):
+        sd = torch.load(checkpoint, map_location="cpu", weights_only=True)
+        own = model.state_dict()
+        own.update({k: v for k, v in sd.items() if k in own})  # net.py:21-34 load_model semantics
+        model.load_state_dict(own)
+    else:
+        model.load_state_dict(seeded_torch_state_dict(seed))
+    dev = device if device is not None else (torch.device("cuda") if torch.cuda.is_available() else None)
+    if dev is not None:
+        model = model.to(dev)
+    return model
+
+
+def get_codec_model(name, loss_type="P", compression_level=2, noMeasure=True, use_split=True, num_views=0,
+                    resilience=0, use_attn=True, load_with_copy=False, **kw):
+    """models.py:32-66 — only the DVC-pretrained codec is built here."""
+    if name in ["DVC-pretrained"]:
+        return get_DVC_pretrained(compression_level, **kw)
+    raise NotImplementedError(f"codec {name!r} is outside this build's scope (DVC-pretrained only)")
+
+
+class AverageMeter(object):
+    """models.py:1414-1430."""
+
+    def __init__(self):
+        self.reset()
+
+    def reset(self):
+        self.val = 0
+        self.avg = 0
+        self.sum = 0
+        self.count = 0
+
+    def update(self, val, n=1):
+        self.val = val
+        self.sum += val * n
+        self.count += n
+        self.avg = self.sum / self.count
+
+
+def PSNR(Y1_raw, Y1_com, use_list=False):
+    """models.py:460-473 (10*ln(1/mse)/ln(10))."""
+    Y1_com = Y1_com.to(Y1_raw.device)
+    log10 = math.log(10.0)
+    if not use_list:
+        train_mse = torch.mean(torch.pow(Y1_raw - Y1_com, 2))
+        return 10.0 * torch.log(1 / train_mse) / log10
+    out = []
+    for i in range(Y1_raw.size(0)):
+        train_mse = torch.mean(torch.pow(Y1_raw[i:i + 1] - Y1_com[i:i + 1], 2))
+        out.append(10.0 * torch.log(1 / train_mse) / log10)
+    return out
+
+
+def I_compression(Y1_raw, I_level, model_name=""):
+    """models.py:412-429 calls bpgenc/bpgdec; BPG is out of scope: lossless pass-through."""
+    return Y1_raw, torch.zeros((), device=Y1_raw.device), torch.full((), float("inf"), device=Y1_raw.device)
+
+
+def _psnr_from_mse(m):
+    return 10.0 * torch.log(1 / m) / math.log(10.0)
+
+
+def parallel_compression(args, model, data, compressI=False, level=0, batch_idx=0):
+    """models.py:233-410 restricted to the DVC-pretrained branch (368-383).
+
+    Returns the reference 11-tuple:
+    (x_hat, loss, img_loss, be_loss, be_res_loss, psnr, psnr_list, aux_loss, aux2, aux3, aux4)."""
+    if model.name != "DVC-pretrained":
+        raise NotImplementedError(model.name)
+    img_loss_list, bpp_list, psnr_list = [], [], []
+    aux_loss_list, aux2_loss_list = [], []
+    x_hat, bpp_i, psnr_i = I_compression(data[0:1], model.I_level)
+    data[0:1] = x_hat
+    if compressI:
+        bpp_list += [bpp_i]
+        psnr_list += [psnr_i]
+    B = data.size(0)
+    x_prev = data[0:1]
+    x_hat_list = []
+    for i in range(1, B):
+        x_prev, mseloss, warploss, interloss, bpp_feature, bpp_z, bpp_mv, bpp = model(data[i:i + 1], x_prev)
+        x_prev = x_prev.detach()
+        img_loss_list += [model.r * mseloss]
+        aux_loss_list += [_psnr_from_mse(warploss)]
+        bpp_list += [bpp]
+        psnr_list += [_psnr_from_mse(mseloss)]
+        aux2_loss_list += [_psnr_from_mse(interloss)]
+        x_hat_list.append(x_prev)
+    x_hat = torch.cat(x_hat_list, dim=0) if x_hat_list else data[0:0]
+    be_loss = torch.stack(bpp_list, 0).mean(0).cpu().item() if bpp_list else 0
+    img_loss = 0  # reference: only set when all_loss_list is non-empty (never for DVC-pretrained)
+    psnr = torch.stack(psnr_list, 0).mean(0).cpu().item() if psnr_list else 0
+    aux_loss = torch.stack(aux_loss_list, 0).mean(0).cpu().item() if aux_loss_list else 0
+    aux2_loss = torch.stack(aux2_loss_list, 0).mean(0).cpu().item() if aux2_loss_list else 0
+    psnrs = torch.stack(psnr_list, 0).tolist() if psnr_list else []
+    return x_hat, 0, img_loss, be_loss, 0, psnr, psnrs, aux_loss, aux2_loss, 0, 0

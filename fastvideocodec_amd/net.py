@@ -1,0 +1,482 @@
+"""DVC P-frame codec (``DVC/net.py:VideoCompressor``) on the libfvc HIP kernels.
+
+Module tree, parameter names and shapes mirror the reference exactly
+(``DVC/net.py:38-57`` and ``DVC/subnet/*``) so ``state_dict``s are interchangeable; the
+forward is a straight-line schedule of HIP kernels over NHWC activations:
+
+  SpyNet (4 levels x [assemble, 5 conv7x7])  -> estmv
+  mvEncoder (8 conv3x3)                      -> mvfeature        (round fused downstream)
+  mvDecoder (4 deconv + 4 conv, in_op=round) -> quant_mv_upsample
+  mc_assemble + Warp_net (13 conv3x3, pool/upsample skips) + warpframe -> prediction
+  resEncoder (conv5x5 s2 + GDN) x4           -> feature
+  respriorEncoder (abs fused) / respriorDecoder (round fused, exp fused) -> recon_sigma
+  resDecoder (deconv5x5 s2 + IGDN, round fused, + prediction fused) -> recon
+  recon_finalize (clamp + 3 SSE reductions), Laplace/BitEstimator bit reductions.
+
+``forward`` returns the reference 8-tuple. ``compress``/``decompress`` add the real range
+coder (the reference's DVC path only estimates bits unless ``calrealbits``, net.py:57).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+import torch.nn as nn
+from torch.nn import Parameter
+
+from . import kernels as K
+from .entropy_models import FactorizedTables, LaplaceTables, RangeCoder, get_scale_table
+from .weights import OUT_CHANNEL_M, OUT_CHANNEL_MV, OUT_CHANNEL_N
+
+
+# ------------------------------------------------------------------ parameter holders
+class _ConvP(nn.Module):
+    """Parameters of an nn.Conv2d / nn.ConvTranspose2d (same names/shapes as torch)."""
+
+    def __init__(self, cin, cout, k, stride=1, transposed=False):
+        super().__init__()
+        shape = (cin, cout, k, k) if transposed else (cout, cin, k, k)
+        self.weight = Parameter(torch.zeros(shape), requires_grad=False)
+        self.bias = Parameter(torch.zeros(cout), requires_grad=False)
+        self.k, self.stride, self.transposed = k, stride, transposed
+        self._packed = None
+
+    def packed(self) -> K.PackedConv:
+        if self._packed is None:
+            self._packed = K.PackedConv(self.weight, self.bias, self.k, self.stride, self.transposed,
+                                        self.weight.device)
+        return self._packed
+
+    def invalidate(self):
+        self._packed = None
+
+
+class _GDNP(nn.Module):
+    """GDN parameters (GDN.py:45-61) and their effective values (GDN.py:75-84)."""
+
+    def __init__(self, ch, inverse=False):
+        super().__init__()
+        self.inverse = inverse
+        self.beta = Parameter(torch.ones(ch), requires_grad=False)
+        self.gamma = Parameter(torch.eye(ch), requires_grad=False)
+        self._eff = None
+
+    def effective(self):
+        if self._eff is None:
+            pedestal = np.float32((2.0 ** -18) ** 2)
+            beta_bound = np.float32((1e-6 + float(pedestal)) ** 0.5)
+            gamma_bound = np.float32(2.0 ** -18)
+            b = self.beta.detach().cpu().numpy().astype(np.float32)
+            g = self.gamma.detach().cpu().numpy().astype(np.float32)
+            b = np.maximum(b, beta_bound) ** 2 - pedestal
+            g = np.maximum(g, gamma_bound) ** 2 - pedestal
+            dev = self.beta.device
+            self._eff = (torch.from_numpy(b.astype(np.float32)).to(dev),
+                         torch.from_numpy(np.ascontiguousarray(g, np.float32)).to(dev))
+        return self._eff
+
+    def invalidate(self):
+        self._eff = None
+
+
+class Bitparm(nn.Module):
+    def __init__(self, channel, final=False):
+        super().__init__()
+        self.final = final
+        self.h = Parameter(torch.zeros(1, channel, 1, 1), requires_grad=False)
+        self.b = Parameter(torch.zeros(1, channel, 1, 1), requires_grad=False)
+        self.a = None if final else Parameter(torch.zeros(1, channel, 1, 1), requires_grad=False)
+
+
+class BitEstimator(nn.Module):
+    """bitEstimator.py:27-42 parameters; evaluated by fvc_bits_factorized / the CDF tables."""
+
+    def __init__(self, channel):
+        super().__init__()
+        self.channel = channel
+        self.f1, self.f2, self.f3 = Bitparm(channel), Bitparm(channel), Bitparm(channel)
+        self.f4 = Bitparm(channel, True)
+
+    def params(self) -> torch.Tensor:
+        rows = []
+        for f in (self.f1, self.f2, self.f3):
+            rows += [f.h.view(-1), f.b.view(-1), f.a.view(-1)]
+        rows += [self.f4.h.view(-1), self.f4.b.view(-1)]
+        return torch.stack(rows, 0).detach().contiguous()
+
+
+# ------------------------------------------------------------------ sub-networks
+class MEBasic(nn.Module):
+    """endecoder.py:142-169: 5x conv7x7 8->32->64->32->16->2."""
+
+    def __init__(self):
+        super().__init__()
+        ch = [8, 32, 64, 32, 16, 2]
+        for i in range(5):
+            setattr(self, f"conv{i+1}", _ConvP(ch[i], ch[i + 1], 7))
+
+    def run(self, x8, flow_up):
+        x = self.conv1.packed()(x8, act=K.ACT_RELU)
+        x = self.conv2.packed()(x, act=K.ACT_RELU)
+        x = self.conv3.packed()(x, act=K.ACT_RELU)
+        x = self.conv4.packed()(x, act=K.ACT_RELU)
+        return self.conv5.packed()(x, res=flow_up)  # flow = flow_up + MEBasic(...) (endecoder.py:354)
+
+
+class ME_Spynet(nn.Module):
+    """endecoder.py:312-356."""
+
+    def __init__(self):
+        super().__init__()
+        self.L = 4
+        self.moduleBasic = nn.ModuleList([MEBasic() for _ in range(4)])
+
+    def run(self, im1, im2):
+        im1l, im2l = [im1], [im2]
+        for lvl in range(self.L - 1):
+            im1l.append(K.avgpool2(im1l[lvl]))
+            im2l.append(K.avgpool2(im2l[lvl]))
+        flow = None  # zeros at 1/16 (endecoder.py:348-351)
+        for lvl in range(self.L):
+            i = self.L - 1 - lvl
+            flow_up, x8 = K.spynet_assemble(im1l[i], im2l[i], flow)
+            flow = self.moduleBasic[lvl].run(x8, flow_up)
+        return flow
+
+
+class Analysis_mv_net(nn.Module):
+    """analysis_mv.py:8-66."""
+
+    def __init__(self):
+        super().__init__()
+        mv = OUT_CHANNEL_MV
+        for i in range(1, 9):
+            setattr(self, f"conv{i}", _ConvP(2 if i == 1 else mv, mv, 3, 2 if i % 2 == 1 else 1))
+
+    def run(self, x):
+        for i in range(1, 9):
+            x = getattr(self, f"conv{i}").packed()(x, act=K.ACT_LRELU if i < 8 else K.ACT_NONE)
+        return x
+
+
+class Synthesis_mv_net(nn.Module):
+    """synthesis_mv.py:9-79; consumes round(mvfeature) (net.py:76) via in_op=round."""
+
+    def __init__(self):
+        super().__init__()
+        mv = OUT_CHANNEL_MV
+        for i in range(1, 9):
+            cout = 2 if i == 8 else mv
+            setattr(self, f"deconv{i}", _ConvP(mv, cout, 3, 2 if i % 2 == 1 else 1, transposed=(i % 2 == 1)))
+
+    def run(self, q):
+        x = q
+        for i in range(1, 9):
+            x = getattr(self, f"deconv{i}").packed()(x, in_op=K.IN_ROUND if i == 1 else K.IN_NONE,
+                                                     act=K.ACT_LRELU if i < 8 else K.ACT_NONE)
+        return x
+
+
+class ResBlock(nn.Module):
+    """endecoder.py:228-260 (pre-activation, identity skip: cin == cout)."""
+
+    def __init__(self, ch=64):
+        super().__init__()
+        self.conv1 = _ConvP(ch, ch, 3)
+        self.conv2 = _ConvP(ch, ch, 3)
+
+    def run(self, x):
+        y = self.conv1.packed()(x, in_op=K.IN_RELU, act=K.ACT_RELU)
+        return self.conv2.packed()(y, res=x)
+
+
+class Warp_net(nn.Module):
+    """endecoder.py:262-296."""
+
+    def __init__(self):
+        super().__init__()
+        self.feature_ext = _ConvP(6, 64, 3)
+        for i in range(6):
+            setattr(self, f"conv{i}", ResBlock(64))
+        self.conv6 = _ConvP(64, 3, 3)
+
+    def run(self, x8, warpframe):
+        fe = self.feature_ext.packed()(x8, act=K.ACT_RELU)
+        c0 = self.conv0.run(fe)
+        c1 = self.conv1.run(K.avgpool2(c0))
+        c2 = self.conv2.run(K.avgpool2(c1))
+        c3 = self.conv3.run(c2)
+        c3u = K.upsample2x_add(c3, skip=c1, align_corners=True)
+        c4 = self.conv4.run(c3u)
+        c4u = K.upsample2x_add(c4, skip=c0, align_corners=True)
+        c5 = self.conv5.run(c4u)
+        return self.conv6.packed()(c5, res=warpframe)  # prediction = warpnet(...) + warpframe (net.py:67)
+
+
+class Analysis_net(nn.Module):
+    """analysis.py:10-48."""
+
+    def __init__(self):
+        super().__init__()
+        N, M = OUT_CHANNEL_N, OUT_CHANNEL_M
+        cins, couts = [3, N, N, N], [N, N, N, M]
+        for i in range(4):
+            setattr(self, f"conv{i+1}", _ConvP(cins[i], couts[i], 5, 2))
+            if i < 3:
+                setattr(self, f"gdn{i+1}", _GDNP(N))
+
+    def run(self, x):
+        for i in range(1, 5):
+            x = getattr(self, f"conv{i}").packed()(x)
+            if i < 4:
+                b, g = getattr(self, f"gdn{i}").effective()
+                x = K.gdn(x, b, g, False)
+        return x
+
+
+class Synthesis_net(nn.Module):
+    """synthesis.py:8-58; input round(feature) via in_op=round; + prediction fused."""
+
+    def __init__(self):
+        super().__init__()
+        N, M = OUT_CHANNEL_N, OUT_CHANNEL_M
+        cins, couts = [M, N, N, N], [N, N, N, 3]
+        for i in range(4):
+            setattr(self, f"deconv{i+1}", _ConvP(cins[i], couts[i], 5, 2, transposed=True))
+            if i < 3:
+                setattr(self, f"igdn{i+1}", _GDNP(N, inverse=True))
+
+    def run(self, feature, prediction):
+        x = feature
+        for i in range(1, 5):
+            x = getattr(self, f"deconv{i}").packed()(x, in_op=K.IN_ROUND if i == 1 else K.IN_NONE,
+                                                     res=prediction if i == 4 else None)
+            if i < 4:
+                b, g = getattr(self, f"igdn{i}").effective()
+                x = K.gdn(x, b, g, True)
+        return x
+
+
+class Analysis_prior_net(nn.Module):
+    """analysis_prior.py:10-56 (abs fused into conv1 staging)."""
+
+    def __init__(self):
+        super().__init__()
+        N, M = OUT_CHANNEL_N, OUT_CHANNEL_M
+        self.conv1 = _ConvP(M, N, 3)
+        self.conv2 = _ConvP(N, N, 5, 2)
+        self.conv3 = _ConvP(N, N, 5, 2)
+
+    def run(self, x):
+        x = self.conv1.packed()(x, in_op=K.IN_ABS, act=K.ACT_RELU)
+        x = self.conv2.packed()(x, act=K.ACT_RELU)
+        return self.conv3.packed()(x)
+
+
+class Synthesis_prior_net(nn.Module):
+    """synthesis_prior.py:11-58 (round(z) fused into deconv1 staging, exp fused into deconv3)."""
+
+    def __init__(self):
+        super().__init__()
+        N, M = OUT_CHANNEL_N, OUT_CHANNEL_M
+        self.deconv1 = _ConvP(N, N, 5, 2, transposed=True)
+        self.deconv2 = _ConvP(N, N, 5, 2, transposed=True)
+        self.deconv3 = _ConvP(N, M, 3, 1, transposed=True)
+
+    def run(self, z):
+        x = self.deconv1.packed()(z, in_op=K.IN_ROUND, act=K.ACT_RELU)
+        x = self.deconv2.packed()(x, act=K.ACT_RELU)
+        return self.deconv3.packed()(x, post=K.POST_EXP)
+
+
+# ------------------------------------------------------------------ the codec
+class PFrameBitstream:
+    """In-memory P-frame bitstream: three latents, one rANS stream per (frame, channel)."""
+
+    def __init__(self, mv, z, feature, batch, hw16, hw64):
+        self.mv, self.z, self.feature = mv, z, feature
+        self.batch, self.hw16, self.hw64 = batch, hw16, hw64
+
+    def nbytes(self) -> int:
+        return int((self.mv.pack_off[-1] + self.z.pack_off[-1] + self.feature.pack_off[-1]).item()) * 4
+
+
+class VideoCompressor(nn.Module):
+    """DVC/net.py:38-220 — same submodule names, same forward contract."""
+
+    def __init__(self):
+        super().__init__()
+        self.opticFlow = ME_Spynet()
+        self.mvEncoder = Analysis_mv_net()
+        self.Q = None
+        self.mvDecoder = Synthesis_mv_net()
+        self.warpnet = Warp_net()
+        self.resEncoder = Analysis_net()
+        self.resDecoder = Synthesis_net()
+        self.respriorEncoder = Analysis_prior_net()
+        self.respriorDecoder = Synthesis_prior_net()
+        self.bitEstimator_z = BitEstimator(OUT_CHANNEL_N)
+        self.bitEstimator_mv = BitEstimator(OUT_CHANNEL_MV)
+        self.warp_weight = 0
+        self.mxrange = 150
+        self.calrealbits = False
+        self._coders = None
+        self.eval()
+
+    # -- cache invalidation when weights/device change
+    def _apply(self, fn, *args, **kwargs):
+        r = super()._apply(fn, *args, **kwargs)
+        self.invalidate()
+        return r
+
+    def load_state_dict(self, *args, **kwargs):
+        r = super().load_state_dict(*args, **kwargs)
+        self.invalidate()
+        return r
+
+    def invalidate(self):
+        for m in self.modules():
+            if isinstance(m, (_ConvP, _GDNP)):
+                m.invalidate()
+        self._coders = None
+        self._be = None
+
+    def _be_params(self):
+        if getattr(self, "_be", None) is None:
+            self._be = (self.bitEstimator_z.params(), self.bitEstimator_mv.params())
+        return self._be
+
+    # -- entropy coders (EntropyBottleneck/GaussianConditional.update(force=True) analogue)
+    def update(self, force=False):
+        if self._coders is not None and not force:
+            return False
+        dev = self.bitEstimator_z.f1.h.device
+        bz, bmv = (p.cpu().numpy() for p in self._be_params())
+        tz, tmv, tf = FactorizedTables(bz), FactorizedTables(bmv), LaplaceTables()
+        self._coders = {
+            "z": RangeCoder(tz.cdf, tz.cdf_length, tz.offset, dev),
+            "mv": RangeCoder(tmv.cdf, tmv.cdf_length, tmv.offset, dev),
+            "feature": RangeCoder(tf.cdf, tf.cdf_length, tf.offset, dev),
+            "scale_table": torch.from_numpy(tf.scale_table).to(dev),
+            "tables": (tz, tmv, tf),
+        }
+        return True
+
+    def motioncompensation(self, ref4, mv4):
+        """net.py:64-68 on NHWC tensors: returns (prediction, warpframe)."""
+        warpframe, x8 = K.mc_assemble(ref4, mv4)
+        prediction = self.warpnet.run(x8, warpframe)
+        return prediction, warpframe
+
+    @staticmethod
+    def _check_frames(input_image, referframe):
+        if input_image.dim() != 4 or input_image.shape[1] != 3 or input_image.shape != referframe.shape:
+            raise ValueError("expected [B,3,H,W] frames of equal shape")
+        B, _, H, W = input_image.shape
+        if H % 64 or W % 64:
+            raise ValueError(f"H and W must be multiples of 64 (got {H}x{W}); replicate-pad first")
+        if not input_image.is_cuda:
+            raise ValueError("VideoCompressor runs on the GPU (libfvc); move the model and frames to cuda")
+
+    def _encode_graph(self, input_image, referframe):
+        """The full encoder-side forward on NHWC tensors; returns a dict of device tensors."""
+        cur4 = K.nchw_to_nhwc(input_image.float().contiguous(), 4)
+        ref4 = K.nchw_to_nhwc(referframe.float().contiguous(), 4)
+        estmv = self.opticFlow.run(cur4, ref4)
+        mvfeature = self.mvEncoder.run(estmv)
+        mv_up = self.mvDecoder.run(mvfeature)
+        prediction, warpframe = self.motioncompensation(ref4, mv_up)
+        residual = K.sub(cur4, prediction)
+        feature = self.resEncoder.run(residual)
+        z = self.respriorEncoder.run(feature)
+        sigma = self.respriorDecoder.run(z)
+        recon = self.resDecoder.run(feature, prediction)
+        return dict(cur4=cur4, ref4=ref4, estmv=estmv, mvfeature=mvfeature, mv_up=mv_up,
+                    prediction=prediction, warpframe=warpframe, feature=feature, z=z, sigma=sigma,
+                    recon=recon)
+
+    def forward(self, input_image, referframe, quant_noise_feature=None, quant_noise_z=None,
+                quant_noise_mv=None, return_intermediates=False):
+        if self.training:
+            raise NotImplementedError("training-mode forward (additive quantisation noise) is out of scope")
+        self._check_frames(input_image, referframe)
+        with torch.no_grad():
+            t = self._encode_graph(input_image, referframe)
+            B, _, H, W = input_image.shape
+            clipped, sse = K.recon_finalize(t["recon"], t["cur4"], t["warpframe"], t["prediction"])
+            npx = B * H * W
+            if self.calrealbits:
+                bs = self.compress_tensors(t)
+                bits_f = bs.feature.pack_off[-1:].double() * 32
+                bits_z = bs.z.pack_off[-1:].double() * 32
+                bits_mv = bs.mv.pack_off[-1:].double() * 32
+            else:
+                bz, bmv = self._be_params()
+                bits_f = K.bits_laplace(t["feature"], t["sigma"], OUT_CHANNEL_M)
+                bits_z = K.bits_factorized(t["z"], bz, OUT_CHANNEL_N)
+                bits_mv = K.bits_factorized(t["mvfeature"], bmv, OUT_CHANNEL_MV)
+            mse_loss = (sse[0] / (3 * npx)).float()
+            warploss = (sse[1] / (3 * npx)).float()
+            interloss = (sse[2] / (3 * npx)).float()
+            bpp_feature = (bits_f[0] / npx).float()
+            bpp_z = (bits_z[0] / npx).float()
+            bpp_mv = (bits_mv[0] / npx).float()
+            bpp = bpp_feature + bpp_z + bpp_mv
+        out = (clipped, mse_loss, warploss, interloss, bpp_feature, bpp_z, bpp_mv, bpp)
+        if return_intermediates:
+            return out, t
+        return out
+
+    # ---------------------------------------------------------------- real bitstream
+    def compress_tensors(self, t) -> PFrameBitstream:
+        self.update()
+        c = self._coders
+        B, H16, W16, _ = t["mvfeature"].shape
+        H64, W64 = t["z"].shape[1:3]
+        sym_mv = K.latent_to_symbols(t["mvfeature"], OUT_CHANNEL_MV)
+        sym_z = K.latent_to_symbols(t["z"], OUT_CHANNEL_N)
+        sym_f = K.latent_to_symbols(t["feature"], OUT_CHANNEL_M)
+        idx_mv = K.channel_indexes(B, H16 * W16, OUT_CHANNEL_MV, sym_mv.device)
+        idx_z = K.channel_indexes(B, H64 * W64, OUT_CHANNEL_N, sym_z.device)
+        idx_f = K.build_indexes(t["sigma"], c["scale_table"], OUT_CHANNEL_M)
+        enc_mv = c["mv"].encode(sym_mv.view(-1, H16 * W16), idx_mv.view(-1, H16 * W16))
+        enc_z = c["z"].encode(sym_z.view(-1, H64 * W64), idx_z.view(-1, H64 * W64))
+        enc_f = c["feature"].encode(sym_f.view(-1, H16 * W16), idx_f.view(-1, H16 * W16))
+        return PFrameBitstream(enc_mv, enc_z, enc_f, B, (H16, W16), (H64, W64))
+
+    def compress(self, input_image, referframe, return_sse=False):
+        """Encode one P-frame: returns (bitstream, clipped_recon[, sse]). The recon is what
+        ``decompress`` reproduces bit-for-bit; sse = device doubles {recon, warp, pred} SSE."""
+        self._check_frames(input_image, referframe)
+        with torch.no_grad():
+            t = self._encode_graph(input_image, referframe)
+            bs = self.compress_tensors(t)
+            clipped, sse = K.recon_finalize(t["recon"], t["cur4"], t["warpframe"], t["prediction"])
+        if return_sse:
+            return bs, clipped, sse
+        return bs, clipped
+
+    def decompress(self, bs: PFrameBitstream, referframe, check=True):
+        """Decode a P-frame from its bitstream and the reference frame (z -> sigma -> feature;
+        mv -> motion compensation; residual synthesis)."""
+        self.update()
+        c = self._coders
+        B = bs.batch
+        (H16, W16), (H64, W64) = bs.hw16, bs.hw64
+        dev = referframe.device
+        with torch.no_grad():
+            ref4 = K.nchw_to_nhwc(referframe.float().contiguous(), 4)
+            idx_z = K.channel_indexes(B, H64 * W64, OUT_CHANNEL_N, dev)
+            sym_z = c["z"].decode(bs.z, idx_z.view(-1, H64 * W64), check).view(B, OUT_CHANNEL_N, H64 * W64)
+            z = K.symbols_to_latent(sym_z, H64, W64, OUT_CHANNEL_N)
+            sigma = self.respriorDecoder.run(z)
+            idx_f = K.build_indexes(sigma, c["scale_table"], OUT_CHANNEL_M)
+            sym_f = c["feature"].decode(bs.feature, idx_f.view(-1, H16 * W16), check).view(B, OUT_CHANNEL_M, H16 * W16)
+            feature = K.symbols_to_latent(sym_f, H16, W16, OUT_CHANNEL_M)
+            idx_mv = K.channel_indexes(B, H16 * W16, OUT_CHANNEL_MV, dev)
+            sym_mv = c["mv"].decode(bs.mv, idx_mv.view(-1, H16 * W16), check).view(B, OUT_CHANNEL_MV, H16 * W16)
+            mvq = K.symbols_to_latent(sym_mv, H16, W16, OUT_CHANNEL_MV)
+            mv_up = self.mvDecoder.run(mvq)
+            prediction, warpframe = self.motioncompensation(ref4, mv_up)
+            recon = self.resDecoder.run(feature, prediction)
+            clipped = K.nhwc_to_nchw(recon, 3, clamp01=True)
+        return clipped

@@ -1,0 +1,45 @@
+"""Live per-kernel timing with HIP events on the launching stream (used by bench.py).
+
+When a ``KernelTimer`` is active, every ``PackedConv`` launch records a start/end
+``torch.cuda.Event`` pair on the current stream (the stream the kernel is launched on) and
+the algorithmic FLOPs of that launch. Events only; no host synchronisation until ``collect``.
+"""
+from __future__ import annotations
+
+import torch
+
+_ACTIVE = None
+
+
+def conv_flops(cin, cout, k, stride, transposed, batch, h, w):
+    """Algorithmic FLOPs (2 x MAC, unpadded channels) of one conv / deconv launch."""
+    if transposed:
+        # every input pixel scatters k*k taps into the output: MAC = B*h*w*cin*cout*k*k
+        return 2.0 * batch * h * w * cin * cout * k * k
+    ho, wo = h // stride, w // stride
+    return 2.0 * batch * ho * wo * cin * cout * k * k
+
+
+class KernelTimer:
+    def __init__(self):
+        self.records = []
+
+    def __enter__(self):
+        global _ACTIVE
+        _ACTIVE = self
+        return self
+
+    def __exit__(self, *exc):
+        global _ACTIVE
+        _ACTIVE = None
+
+    def collect(self):
+        """Synchronise and return (total_ms, total_flops, n_launches)."""
+        torch.cuda.synchronize()
+        ms = sum(s.elapsed_time(e) for s, e, _ in self.records)
+        fl = sum(f for _, _, f in self.records)
+        return ms, fl, len(self.records)
+
+
+def active():
+    return _ACTIVE

@@ -1,0 +1,164 @@
+/*
+ * libfvc — MI355X (gfx950) C-ABI for the DVC P-frame encode/decode hot path.
+ *
+ * Every entry point is `extern "C"`, takes plain pointers + sizes + a hipStream_t, never
+ * allocates, never throws, and returns 0 on success or a negative code
+ * (-hipError_t, or FVC_E*). Device pointers are caller-owned (torch tensors in the Python
+ * host layer); calls are stream-ordered and reentrant per stream.
+ *
+ * Activation layout inside the codec is NHWC fp32 with the channel count padded to a
+ * multiple of 4 ("cp"; pad channels are written as zeros). Frames at the module boundary
+ * are NCHW fp32, exactly as the reference forward takes them.
+ *
+ * Reference interfaces replaced (paths relative to the reference repo):
+ *   conv/deconv .......... nn.Conv2d / nn.ConvTranspose2d of DVC/subnet/{endecoder,analysis*,
+ *                          synthesis*}.py (ATen conv2d / conv_transpose2d)
+ *   warp ................. endecoder.py:52-67 torch_warp / :116-119 flow_warp (grid_sample)
+ *   upsample ............. endecoder.py:173-184 bilinearupsacling(2)  (upsample_bilinear2d)
+ *   avgpool .............. endecoder.py:345-346, :272,274               (avg_pool2d)
+ *   gdn .................. DVC/subnet/GDN.py:63-93
+ *   bits ................. DVC/net.py:121-205 (Laplace + BitEstimator estimates)
+ *   indexes .............. compressai GaussianConditional.build_indexes (entropy_models.py:82,90)
+ *   rans ................. compressai RansEncoder/RansDecoder.{encode,decode}_with_indexes
+ *                          (pybind11, called from entropy_models.py:82-93)
+ *   pmf_to_quantized_cdf . compressai._CXX.pmf_to_quantized_cdf (EntropyModel._pmf_to_cdf)
+ */
+#ifndef FVC_H_
+#define FVC_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ihipStream_t* fvc_stream_t; /* == hipStream_t */
+
+enum {
+  FVC_OK = 0,
+  FVC_EINVAL = -1000,  /* bad shape / argument */
+  FVC_ENOSPC = -1001,  /* output capacity too small */
+  FVC_ECORRUPT = -1002 /* malformed bitstream */
+};
+
+/* conv input transform applied while staging the input tile */
+enum { FVC_IN_NONE = 0, FVC_IN_RELU = 1, FVC_IN_ABS = 2, FVC_IN_ROUND = 3 };
+/* activation after bias */
+enum { FVC_ACT_NONE = 0, FVC_ACT_RELU = 1, FVC_ACT_LRELU = 2 /* slope 0.1 */ };
+/* transform after the residual add */
+enum { FVC_POST_NONE = 0, FVC_POST_EXP = 1 };
+
+int fvc_version(void);
+int fvc_device_arch_ok(void); /* 1 if device 0 is gfx950 */
+
+/* ------------------------------------------------------------------ convolutions
+ * y = post( act(conv(in_op(x)) + bias) + res )
+ * conv:   nn.Conv2d(cin, cout, k, stride, padding=k//2)              -> out h/stride x w/stride
+ * deconv: nn.ConvTranspose2d(cin, cout, k, stride, padding=k//2,
+ *                            output_padding=stride-1)                 -> out h*stride x w*stride
+ * Weights come in the reference layout (conv OIHW, deconv IOHW) on the HOST and are packed
+ * once by fvc_conv_pack_weight into the kernel's k-block layout (copy the pack to device).
+ * res may be NULL. x: [b][h][w][cp_in]; y: [b][ho][wo][cp_out]; res like y.
+ */
+size_t fvc_conv_wpack_floats(int cin, int cout, int ksize, int stride, int transposed);
+int fvc_conv_pack_weight(const float* w_host, float* wpack_host, int cin, int cout, int ksize,
+                         int stride, int transposed);
+int fvc_conv2d_nhwc_f32(const float* x, const float* wpack, const float* bias, const float* res,
+                        float* y, int batch, int h, int w, int cin, int cout, int ksize, int stride,
+                        int in_op, int act, int post_op, fvc_stream_t stream);
+int fvc_deconv2d_nhwc_f32(const float* x, const float* wpack, const float* bias,
+                          const float* res, float* y, int batch, int h, int w, int cin, int cout,
+                          int ksize, int stride, int in_op, int act, int post_op,
+                          fvc_stream_t stream);
+
+/* ------------------------------------------------------------------ layout / resampling */
+int fvc_nchw_to_nhwc(const float* src, float* dst, int batch, int c, int h, int w, int cp,
+                     fvc_stream_t stream);
+/* clamp01: also clamp to [0,1] (the decoder's final recon.clamp(0,1), net.py:105) */
+int fvc_nhwc_to_nchw(const float* src, float* dst, int batch, int c, int h, int w, int cp,
+                     int clamp01, fvc_stream_t stream);
+/* 2x2 mean, src h x w (even) -> h/2 x w/2 */
+int fvc_avgpool2_nhwc(const float* src, float* dst, int batch, int h, int w, int cp,
+                      fvc_stream_t stream);
+/* backward bilinear warp, border padding (torch_warp), im/out [b][h][w][cp], flow [b][h][w][4] */
+int fvc_warp_nhwc(const float* im, const float* flow, float* out, int batch, int h, int w, int cp,
+                  fvc_stream_t stream);
+/* out = skip + upsample2x(src) ; src h x w -> 2h x 2w ; align_corners 0/1 ; scale multiplies
+ * the upsampled value (SpyNet uses 2.0, ac=0); skip may be NULL */
+int fvc_upsample2x_add_nhwc(const float* src, const float* skip, float* out, int batch, int h,
+                            int w, int cp, int align_corners, float scale, fvc_stream_t stream);
+/* SpyNet level input (endecoder.py:352-354): flow_up = 2*up2(flow_prev) (flow_prev may be NULL
+ * = zeros); x8 = [im1, warp(im2, flow_up), flow_up]; im1/im2 [b][h][w][4], flow [b][h][w][4],
+ * x8 [b][h][w][8] */
+int fvc_spynet_assemble(const float* im1, const float* im2, const float* flow_prev,
+                        float* flow_up, float* x8, int batch, int h, int w, fvc_stream_t stream);
+/* motion compensation input (net.py:64-68): warpframe = warp(ref, mv); x8 = [warpframe, ref, 0, 0] */
+int fvc_mc_assemble(const float* ref, const float* mv, float* warpframe, float* x8, int batch,
+                    int h, int w, fvc_stream_t stream);
+/* out = a - b elementwise over n floats */
+int fvc_sub_f32(const float* a, const float* b, float* out, size_t n, fvc_stream_t stream);
+
+/* ------------------------------------------------------------------ GDN (GDN.py:63-93)
+ * beta/gamma are the effective (bounded, reparametrised) parameters: gamma[i*c + j] */
+int fvc_gdn_nhwc(const float* x, float* y, const float* beta, const float* gamma, int batch,
+                 int h, int w, int c, int inverse, fvc_stream_t stream);
+
+/* ------------------------------------------------------------------ reductions
+ * Deterministic (fixed-order, no atomics) two-pass reductions; ws must hold
+ * fvc_reduce_ws_doubles() doubles. Results are written to device doubles. */
+size_t fvc_reduce_ws_doubles(void);
+/* clipped = clamp(recon,0,1) as NCHW [b][3][h][w]; out3 = {sum (recon-in)^2, sum (warp-in)^2,
+ * sum (pred-in)^2} over b*3*h*w elements (all inputs NHWC cp=4) */
+int fvc_recon_finalize(const float* recon, const float* input, const float* warpframe,
+                       const float* prediction, float* clipped_nchw, double* out3, double* ws,
+                       int batch, int h, int w, fvc_stream_t stream);
+/* bits of round(feature) under Laplace(0, clamp(sigma,1e-5,1e10)) (net.py:121-151) */
+int fvc_bits_laplace(const float* feature, const float* sigma, double* out1, double* ws,
+                     int batch, int h, int w, int c, int cp, fvc_stream_t stream);
+/* bits of round(v) under the per-channel BitEstimator (net.py:153-205); params [11][c]:
+ * h1 b1 a1 h2 b2 a2 h3 b3 a3 h4 b4 */
+int fvc_bits_factorized(const float* v, const float* params, double* out1, double* ws,
+                        int batch, int h, int w, int c, int cp, fvc_stream_t stream);
+
+/* ------------------------------------------------------------------ entropy coding
+ * Symbol streams are channel-major: stream (b, ch) holds round(lat[b,:,:,ch]) in raster
+ * order. Each stream is coded independently and is byte-identical to compressai's
+ * RansEncoder.encode_with_indexes on that sequence (precision 16, bypass 4 bits). */
+int fvc_latent_to_symbols(const float* lat, int32_t* sym, int batch, int h, int w, int c, int cp,
+                          fvc_stream_t stream);
+int fvc_symbols_to_latent(const int32_t* sym, float* lat, int batch, int h, int w, int c, int cp,
+                          fvc_stream_t stream);
+/* GaussianConditional.build_indexes over a scale table; output channel-major like symbols */
+int fvc_build_indexes(const float* sigma, const float* scale_table, int n_scales, int32_t* idx,
+                      int batch, int h, int w, int c, int cp, fvc_stream_t stream);
+/* per-channel table index for factorized latents: idx[b][ch][i] = ch */
+int fvc_channel_indexes(int32_t* idx, int batch, int hw, int c, fvc_stream_t stream);
+
+/* host: compressai pmf_to_quantized_cdf; cdf_out has n+1 entries. */
+int fvc_pmf_to_quantized_cdf(const float* pmf, int n, int precision, uint32_t* cdf_out);
+
+/* Device rANS over nstreams independent streams. Stream s codes symbols
+ * [sym_off[s], sym_off[s+1]) with tables indexes[i]; cdfs is [ntables][cdf_stride] int32,
+ * cdf_sizes/offsets per table (compressai _quantized_cdf/_cdf_length/_offset).
+ * Encode writes stream s downward into words[word_off[s] .. word_off[s+1]) and its length
+ * (in 32-bit words, counted from the END of its region) into nwords[s]; the stream's bytes are
+ * the last nwords[s] words of its region, little-endian. */
+int fvc_rans_encode(const int32_t* symbols, const int32_t* indexes, const int64_t* sym_off,
+                    int nstreams, const int32_t* cdfs, int cdf_stride, const int32_t* cdf_sizes,
+                    const int32_t* offsets, uint32_t* words, const int64_t* word_off,
+                    int32_t* nwords, fvc_stream_t stream);
+/* Pack encoded regions into one contiguous buffer: out[pack_off[s] ..] = last nwords[s] words
+ * of region s; pack_off is [nstreams+1] (exclusive scan of nwords, computed on device). */
+int fvc_rans_pack(const uint32_t* words, const int64_t* word_off, const int32_t* nwords,
+                  int nstreams, int64_t* pack_off, uint32_t* out, fvc_stream_t stream);
+/* Decode: stream s reads packed words starting at pack_off[s]; status[s] = 0 or FVC_ECORRUPT */
+int fvc_rans_decode(const uint32_t* packed, const int64_t* pack_off, const int32_t* indexes,
+                    const int64_t* sym_off, int nstreams, const int32_t* cdfs, int cdf_stride,
+                    const int32_t* cdf_sizes, const int32_t* offsets, int32_t* symbols,
+                    int32_t* status, fvc_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FVC_H_ */

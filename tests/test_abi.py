@@ -1,0 +1,75 @@
+"""CPU: the C-ABI library builds, loads, exports every symbol include/fvc.h declares, and its
+host-side entry points (weight packing, CDF quantisation) behave. No device calls here."""
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from fastvideocodec_amd import _lib
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_symbols():
+    txt = open(os.path.join(REPO, "include", "fvc.h")).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(fvc_[a-z0-9_]+)\s*\(", txt)))
+
+
+def test_header_matches_binding():
+    assert set(header_symbols()) == set(_lib.EXPORTED)
+
+
+def test_library_exports_every_symbol():
+    lib = _lib.load()
+    for name in header_symbols():
+        assert hasattr(lib, name), name
+    assert lib.fvc_version() >= 1
+
+
+def test_wpack_sizes_and_packing():
+    lib = _lib.load()
+    for cin, cout, k, s, tr in [(8, 32, 7, 1, 0), (128, 128, 3, 2, 1), (64, 3, 5, 2, 1), (64, 96, 3, 1, 1),
+                                (96, 64, 3, 1, 0), (3, 64, 5, 2, 0)]:
+        n = lib.fvc_conv_wpack_floats(cin, cout, k, s, tr)
+        assert n > 0 and n % 128 == 0
+        shape = (cin, cout, k, k) if tr else (cout, cin, k, k)
+        w = torch.randn(shape)
+        out = torch.empty(n)
+        _lib.call("fvc_conv_pack_weight", w.data_ptr(), out.data_ptr(), cin, cout, k, s, tr)
+        # every weight appears exactly once in the pack (the rest is zero padding)
+        assert abs(float(out.abs().sum()) - float(w.abs().sum())) < 1e-3 * float(w.abs().sum())
+        assert int((out != 0).sum()) == int((w != 0).sum())
+    assert lib.fvc_conv_wpack_floats(8, 160, 3, 1, 0) == 0  # > 128 output channels unsupported
+    assert lib.fvc_conv_wpack_floats(8, 16, 4, 1, 0) == 0   # even kernel unsupported
+
+
+def test_pmf_to_quantized_cdf_abi():
+    from fastvideocodec_amd import entropy_models as EM
+    assert EM.pmf_to_quantized_cdf([0.25] * 4).tolist() == [0, 16384, 32768, 49152, 65536]
+    with pytest.raises(_lib.FvcError):
+        EM.pmf_to_quantized_cdf([0.0, 0.0])
+
+
+def test_models_api_surface():
+    from fastvideocodec_amd.models import get_codec_model
+    m = get_codec_model("DVC-pretrained", compression_level=2, device=torch.device("cpu"))
+    assert (m.name, m.compression_level, m.loss_type, m.I_level, m.r) == ("DVC-pretrained", 2, "P", 27, 1024)
+    x = torch.rand(1, 3, 64, 64)
+    with pytest.raises(ValueError):  # no CPU fallback: the product path is HIP-only
+        m(x, x)
+    with pytest.raises(NotImplementedError):
+        get_codec_model("RLVC")
+
+
+def test_state_dict_matches_reference_layout():
+    from fastvideocodec_amd.net import VideoCompressor
+    from fastvideocodec_amd.weights import seeded_state_dict
+    m = VideoCompressor()
+    sd = seeded_state_dict()
+    own = m.state_dict()
+    assert list(own.keys()) == list(sd.keys())
+    for k, v in sd.items():
+        assert tuple(own[k].shape) == v.shape, k

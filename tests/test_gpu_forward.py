@@ -1,0 +1,153 @@
+"""End-to-end parity of the HIP VideoCompressor against the reference golden fixtures
+(produced by the reference DVC forward, tests/golden/gen_golden.py) and the CPU oracle."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from fastvideocodec_amd.models import get_codec_model, parallel_compression, PSNR
+from oracle import dvc_ref
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+# fp32 tolerances (north star: recon within 1e-4 dB PSNR; symbols per SURVEY §7 tiers)
+TOL_TENSOR = 2e-4      # relative to tensor max-abs, per stage
+TOL_PSNR_DB = 1e-4
+TOL_SYMBOL_FLIP = 1e-3  # fraction of symbols allowed to differ at these tiny sizes (expect 0)
+
+
+@pytest.fixture(scope="module")
+def model(dev):
+    return get_codec_model("DVC-pretrained", compression_level=2, device=dev)
+
+
+def nhwc_to_nchw(t, c):
+    return t[..., :c].permute(0, 3, 1, 2).cpu()
+
+
+STAGES = {"estmv": 2, "mvfeature": 128, "mv_up": 2, "warpframe": 3, "prediction": 3, "feature": 96,
+          "z": 64, "sigma": 96}
+GOLD_NAME = {"mv_up": "quant_mv_upsample", "sigma": "recon_sigma"}
+
+
+@pytest.mark.parametrize("size", ["64x64", "128x192", "256x256"])
+def test_forward_vs_golden(model, dev, size):
+    g = np.load(os.path.join(GOLD, f"dvc_{size}.npz"))
+    cur = torch.from_numpy(g["input_image"]).to(dev)
+    ref = torch.from_numpy(g["referframe"]).to(dev)
+    out, t = model(cur, ref, return_intermediates=True)
+    torch.cuda.synchronize()
+    for name, c in STAGES.items():
+        got = nhwc_to_nchw(t[name], c).numpy()
+        exp = g[GOLD_NAME.get(name, name)]
+        scale = np.abs(exp).max() + 1e-6
+        err = np.abs(got - exp).max()
+        assert err <= TOL_TENSOR * scale, f"{name}: {err:.3e} vs {scale:.3e}"
+    for name, gname in (("mvfeature", "quant_mv"), ("feature", "compressed_feature"), ("z", "compressed_z")):
+        got = np.round(nhwc_to_nchw(t[name], STAGES[name]).numpy())
+        flips = float((got != g[gname]).mean())
+        assert flips <= TOL_SYMBOL_FLIP, f"{gname}: flip rate {flips}"
+    names = ["clipped", "mse_loss", "warploss", "interloss", "bpp_feature", "bpp_z", "bpp_mv", "bpp"]
+    for n, o in zip(names, out):
+        o = o.cpu().numpy()
+        exp = g[n]
+        if n == "clipped":
+            assert np.abs(o - exp).max() <= 5e-3
+        else:
+            assert abs(float(o) - float(exp)) <= 2e-4 * abs(float(exp)) + 1e-7, (n, float(o), float(exp))
+    psnr_got = 10 * np.log10(1.0 / float(out[1]))
+    psnr_exp = 10 * np.log10(1.0 / float(g["mse_loss"]))
+    assert abs(psnr_got - psnr_exp) <= TOL_PSNR_DB
+
+
+def test_gop_chain_vs_golden(model, dev):
+    """parallel_compression loop (models.py:368-383) over a 4-frame GOP.
+
+    Open loop (each P-frame coded against the reference's own previous recon) every frame meets
+    the 1e-4 dB bar. Closed loop (our own previous recon) the chain drifts the way the reference
+    drifts across CPU backends (symbol flips propagate through x_prev), so the
+    closed-loop bound is looser and grows with the frame index."""
+    g = np.load(os.path.join(GOLD, "dvc_chain_256x256.npz"))
+    gop = torch.from_numpy(g["gop"]).to(dev)
+    exp_psnr = np.array([10 * np.log10(1 / float(g[f"f{i}_mse_loss"])) for i in range(1, 4)])
+    for i in range(1, 4):
+        ref = gop[0:1] if i == 1 else torch.from_numpy(g[f"f{i-1}_clipped"]).to(dev)
+        out = model(gop[i:i + 1], ref)
+        assert abs(10 * np.log10(1 / float(out[1])) - exp_psnr[i - 1]) <= TOL_PSNR_DB
+        assert abs(float(out[7]) - float(g[f"f{i}_bpp"])) <= 1e-3 * float(g[f"f{i}_bpp"])
+    data = gop.clone()
+    x_hat, loss, img_loss, be_loss, _, psnr, psnr_list, aux, aux2, _, _ = parallel_compression(None, model, data, False)
+    assert x_hat.shape == (3, 3, 256, 256)
+    drift = np.abs(np.array(psnr_list) - exp_psnr)
+    assert drift[0] <= TOL_PSNR_DB and drift.max() <= 2e-2, drift
+    exp_bpp = np.mean([float(g[f"f{i}_bpp"]) for i in range(1, 4)])
+    assert abs(be_loss - exp_bpp) <= 1e-2 * exp_bpp
+
+
+def test_compress_decompress_bitexact(model, dev):
+    g = np.load(os.path.join(GOLD, "dvc_128x192.npz"))
+    cur = torch.from_numpy(g["input_image"]).to(dev)
+    ref = torch.from_numpy(g["referframe"]).to(dev)
+    bs, rec_enc = model.compress(cur, ref)
+    rec_dec = model.decompress(bs, ref)
+    torch.cuda.synchronize()
+    assert torch.equal(rec_enc, rec_dec)
+    assert bs.nbytes() > 0
+    # forward's clipped recon is the same tensor the encoder reconstructs
+    out = model(cur, ref)
+    assert torch.equal(out[0], rec_enc)
+
+
+def test_compress_streams_vs_oracle_coder(model, dev):
+    """Device bitstream == C oracle coder fed the same symbols/indexes/tables."""
+    from oracle import coder_ref as R
+    from fastvideocodec_amd import kernels as K
+    g = np.load(os.path.join(GOLD, "dvc_64x64.npz"))
+    cur = torch.from_numpy(g["input_image"]).to(dev)
+    ref = torch.from_numpy(g["referframe"]).to(dev)
+    with torch.no_grad():
+        t = model._encode_graph(cur, ref)
+    bs = model.compress_tensors(t)
+    tz, tmv, tf = model._coders["tables"]
+    sym_f = K.latent_to_symbols(t["feature"], 96).cpu().numpy().reshape(96, -1)
+    idx_f = K.build_indexes(t["sigma"], model._coders["scale_table"], 96).cpu().numpy().reshape(96, -1)
+    strings = bs.feature.to_bytes_list()
+    for c in range(96):
+        assert strings[c] == R.CRef.encode(sym_f[c], idx_f[c], tf.cdf, tf.cdf_length, tf.offset)
+    sym_mv = K.latent_to_symbols(t["mvfeature"], 128).cpu().numpy().reshape(128, -1)
+    strings = bs.mv.to_bytes_list()
+    for c in range(128):
+        idx = np.full(sym_mv.shape[1], c, np.int32)
+        assert strings[c] == R.CRef.encode(sym_mv[c], idx, tmv.cdf, tmv.cdf_length, tmv.offset)
+
+
+def test_calrealbits(model, dev):
+    g = np.load(os.path.join(GOLD, "dvc_64x64.npz"))
+    cur = torch.from_numpy(g["input_image"]).to(dev)
+    ref = torch.from_numpy(g["referframe"]).to(dev)
+    est = model(cur, ref)
+    model.calrealbits = True
+    try:
+        real = model(cur, ref)
+    finally:
+        model.calrealbits = False
+    # real coded size is within a few percent of the estimate plus per-stream overhead
+    assert float(real[7]) > 0.5 * float(est[7])
+    assert torch.equal(real[0], est[0])
+
+
+def test_batch_matches_single(model, dev):
+    g = np.load(os.path.join(GOLD, "dvc_64x64.npz"))
+    cur = torch.from_numpy(g["input_image"]).to(dev)
+    ref = torch.from_numpy(g["referframe"]).to(dev)
+    one = model(cur, ref)[0]
+    two = model(torch.cat([cur, cur]), torch.cat([ref, ref]))[0]
+    assert torch.equal(two[0:1], one) and torch.equal(two[1:2], one)
+
+
+def test_rejects_bad_sizes(model, dev):
+    x = torch.rand(1, 3, 100, 64, device=dev)
+    with pytest.raises(ValueError):
+        model(x, x)

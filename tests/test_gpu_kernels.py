@@ -1,0 +1,231 @@
+"""Per-kernel parity of libfvc (HIP, cuda:0) against plain PyTorch fp32 CPU references of the
+same op (the ATen ops the reference forward calls) and the coder oracle (byte-exact)."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from fastvideocodec_amd import kernels as K
+from fastvideocodec_amd import entropy_models as EM
+from oracle import coder_ref as R
+from oracle import dvc_ref
+
+pytestmark = pytest.mark.gpu
+
+
+def to_nhwc(x, cp=None):
+    B, C, H, W = x.shape
+    cp = cp or K.cp4(C)
+    y = torch.zeros(B, H, W, cp)
+    y[..., :C] = x.permute(0, 2, 3, 1)
+    return y.contiguous()
+
+
+def from_nhwc(y, c):
+    return y[..., :c].permute(0, 3, 1, 2).contiguous()
+
+
+def close(a, b, tol):
+    scale = float(b.abs().max()) + 1e-6
+    err = float((a - b).abs().max())
+    assert err <= tol * scale + 1e-6, f"max err {err:.3e} vs scale {scale:.3e}"
+
+
+# (cin, cout, k, stride, transposed, H, W, in_op, act, post, with_res)
+CONV_CASES = [
+    (8, 32, 7, 1, False, 36, 70, K.IN_NONE, K.ACT_RELU, K.POST_NONE, False),
+    (32, 64, 7, 1, False, 20, 40, K.IN_NONE, K.ACT_RELU, K.POST_NONE, False),
+    (64, 32, 7, 1, False, 17, 33, K.IN_NONE, K.ACT_RELU, K.POST_NONE, False),
+    (32, 16, 7, 1, False, 16, 32, K.IN_NONE, K.ACT_RELU, K.POST_NONE, False),
+    (16, 2, 7, 1, False, 24, 40, K.IN_NONE, K.ACT_NONE, K.POST_NONE, True),
+    (2, 128, 3, 2, False, 32, 64, K.IN_NONE, K.ACT_LRELU, K.POST_NONE, False),
+    (128, 128, 3, 1, False, 12, 40, K.IN_NONE, K.ACT_LRELU, K.POST_NONE, False),
+    (128, 128, 3, 2, False, 16, 34, K.IN_NONE, K.ACT_LRELU, K.POST_NONE, False),
+    (128, 128, 3, 2, True, 5, 9, K.IN_ROUND, K.ACT_LRELU, K.POST_NONE, False),
+    (128, 2, 3, 1, False, 16, 24, K.IN_NONE, K.ACT_NONE, K.POST_NONE, False),
+    (6, 64, 3, 1, False, 24, 48, K.IN_NONE, K.ACT_RELU, K.POST_NONE, False),
+    (64, 64, 3, 1, False, 19, 45, K.IN_RELU, K.ACT_RELU, K.POST_NONE, True),
+    (64, 3, 3, 1, False, 16, 32, K.IN_NONE, K.ACT_NONE, K.POST_NONE, True),
+    (3, 64, 5, 2, False, 32, 64, K.IN_NONE, K.ACT_NONE, K.POST_NONE, False),
+    (64, 64, 5, 2, False, 16, 70, K.IN_NONE, K.ACT_NONE, K.POST_NONE, False),
+    (64, 96, 5, 2, False, 8, 16, K.IN_NONE, K.ACT_NONE, K.POST_NONE, False),
+    (96, 64, 3, 1, False, 4, 8, K.IN_ABS, K.ACT_RELU, K.POST_NONE, False),
+    (96, 64, 5, 2, True, 4, 6, K.IN_ROUND, K.ACT_NONE, K.POST_NONE, False),
+    (64, 64, 5, 2, True, 8, 12, K.IN_NONE, K.ACT_RELU, K.POST_NONE, False),
+    (64, 3, 5, 2, True, 16, 17, K.IN_NONE, K.ACT_NONE, K.POST_NONE, True),
+    (64, 96, 3, 1, True, 4, 8, K.IN_NONE, K.ACT_NONE, K.POST_EXP, False),
+]
+
+
+def _in_op(x, op):
+    return {K.IN_NONE: x, K.IN_RELU: F.relu(x), K.IN_ABS: x.abs(), K.IN_ROUND: torch.round(x)}[op]
+
+
+@pytest.mark.parametrize("case", CONV_CASES, ids=lambda c: f"ci{c[0]}co{c[1]}k{c[2]}s{c[3]}{'T' if c[4] else ''}")
+def test_conv(dev, case):
+    cin, cout, k, s, tr, H, W, in_op, act, post, with_res = case
+    g = torch.Generator().manual_seed(cin * 1000 + cout + k)
+    x = torch.randn(2, cin, H, W, generator=g) * 2.0
+    wshape = (cin, cout, k, k) if tr else (cout, cin, k, k)
+    w = torch.randn(wshape, generator=g) * (1.0 / (cin * k * k) ** 0.5)
+    b = torch.randn(cout, generator=g) * 0.1
+    xin = _in_op(x, in_op)
+    if tr:
+        ref = F.conv_transpose2d(xin, w, b, s, k // 2, s - 1)
+    else:
+        ref = F.conv2d(xin, w, b, s, k // 2)
+    if act == K.ACT_RELU:
+        ref = F.relu(ref)
+    elif act == K.ACT_LRELU:
+        ref = F.leaky_relu(ref, 0.1)
+    res = torch.randn(ref.shape, generator=g) if with_res else None
+    if res is not None:
+        ref = ref + res
+    if post == K.POST_EXP:
+        ref = torch.exp(ref)
+    pc = K.PackedConv(w, b, k, s, tr, dev)
+    y = pc(to_nhwc(x).to(dev), in_op=in_op, act=act, post=post,
+           res=None if res is None else to_nhwc(res).to(dev))
+    torch.cuda.synchronize()
+    yc = y.cpu()
+    assert yc.shape[1:3] == ref.shape[2:]
+    close(from_nhwc(yc, cout), ref, 2e-5)
+    if K.cp4(cout) > cout:
+        assert float(yc[..., cout:].abs().max()) == 0.0, "pad channels must be zero"
+
+
+def test_conv_deterministic(dev):
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(1, 64, 33, 65, generator=g)
+    w = torch.randn(64, 64, 3, 3, generator=g) * 0.05
+    pc = K.PackedConv(w, torch.zeros(64), 3, 1, False, dev)
+    xd = to_nhwc(x).to(dev)
+    a, b = pc(xd), pc(xd)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
+
+
+def test_warp(dev):
+    g = torch.Generator().manual_seed(1)
+    im = torch.rand(2, 3, 40, 72, generator=g)
+    flow = torch.randn(2, 2, 40, 72, generator=g) * 6.0
+    ref = dvc_ref.warp(im, flow)
+    y = K.warp(to_nhwc(im).to(dev), to_nhwc(flow).to(dev))
+    close(from_nhwc(y.cpu(), 3), ref, 1e-5)
+
+
+@pytest.mark.parametrize("ac", [False, True])
+def test_upsample_add(dev, ac):
+    g = torch.Generator().manual_seed(2)
+    src = torch.randn(2, 64, 9, 15, generator=g)
+    skip = torch.randn(2, 64, 18, 30, generator=g)
+    ref = skip + dvc_ref.up2(src, ac) * (1.0 if ac else 2.0)
+    y = K.upsample2x_add(to_nhwc(src).to(dev), to_nhwc(skip).to(dev), align_corners=ac, scale=1.0 if ac else 2.0)
+    close(from_nhwc(y.cpu(), 64), ref, 1e-6)
+
+
+def test_avgpool(dev):
+    x = torch.randn(2, 64, 18, 34)
+    y = K.avgpool2(to_nhwc(x).to(dev))
+    close(from_nhwc(y.cpu(), 64), F.avg_pool2d(x, 2, 2), 1e-6)
+
+
+def test_spynet_assemble(dev):
+    g = torch.Generator().manual_seed(3)
+    im1, im2 = torch.rand(1, 3, 32, 48, generator=g), torch.rand(1, 3, 32, 48, generator=g)
+    fprev = torch.randn(1, 2, 16, 24, generator=g) * 2
+    fup = dvc_ref.up2(fprev, False) * 2.0
+    ref = torch.cat([im1, dvc_ref.warp(im2, fup), fup], 1)
+    fu, x8 = K.spynet_assemble(to_nhwc(im1).to(dev), to_nhwc(im2).to(dev), to_nhwc(fprev).to(dev))
+    close(from_nhwc(x8.cpu(), 8), ref, 1e-5)
+    close(from_nhwc(fu.cpu(), 2), fup, 1e-6)
+
+
+@pytest.mark.parametrize("inverse", [False, True])
+def test_gdn(dev, seeded_sd, inverse):
+    from fastvideocodec_amd.net import _GDNP
+    g = torch.Generator().manual_seed(4)
+    x = torch.randn(1, 64, 12, 20, generator=g) * 3
+    p = _GDNP(64, inverse).to(dev)
+    with torch.no_grad():
+        p.beta.copy_(torch.rand(64, generator=g) + 0.5)
+        p.gamma.copy_(torch.rand(64, 64, generator=g) * 0.1)
+    sd = {"t.beta": p.beta.cpu(), "t.gamma": p.gamma.cpu()}
+    ref = dvc_ref.gdn(sd, "t", x, inverse)
+    b, gm = p.effective()
+    y = K.gdn(to_nhwc(x).to(dev), b, gm, inverse)
+    close(from_nhwc(y.cpu(), 64), ref, 2e-6)
+
+
+def test_bits(dev, seeded_sd):
+    g = torch.Generator().manual_seed(5)
+    feat = torch.randn(1, 96, 8, 12, generator=g) * 4
+    sigma = torch.exp(torch.randn(1, 96, 8, 12, generator=g))
+    ref = float(dvc_ref.bits_laplace(torch.round(feat), sigma))
+    got = float(K.bits_laplace(to_nhwc(feat).to(dev), to_nhwc(sigma).to(dev), 96).cpu())
+    assert abs(got - ref) <= 1e-4 * abs(ref)
+    from fastvideocodec_amd.net import BitEstimator
+    be = BitEstimator(128)
+    be.load_state_dict({k[len("bitEstimator_mv."):]: v for k, v in seeded_sd.items() if k.startswith("bitEstimator_mv.")})
+    v = torch.randn(1, 128, 8, 12, generator=g) * 5
+    ref = float(dvc_ref.bits_factorized(seeded_sd, "bitEstimator_mv", torch.round(v)))
+    got = float(K.bits_factorized(to_nhwc(v).to(dev), be.params().to(dev), 128).cpu())
+    assert abs(got - ref) <= 1e-4 * abs(ref)
+
+
+def test_recon_finalize(dev):
+    g = torch.Generator().manual_seed(6)
+    r, x, w, p = (torch.rand(2, 3, 16, 24, generator=g) * 1.4 - 0.2 for _ in range(4))
+    clipped, sse = K.recon_finalize(*(to_nhwc(t).to(dev) for t in (r, x, w, p)))
+    assert torch.equal(clipped.cpu(), r.clamp(0, 1))
+    for i, t in enumerate((r, w, p)):
+        assert abs(float(sse[i]) - float(((t.double() - x.double()) ** 2).sum())) < 1e-9 * float(((t - x) ** 2).sum()) + 1e-6
+
+
+def test_symbols_and_indexes(dev):
+    g = torch.Generator().manual_seed(8)
+    lat = torch.randn(2, 96, 6, 10, generator=g) * 7
+    sym = K.latent_to_symbols(to_nhwc(lat).to(dev), 96).cpu()
+    assert torch.equal(sym, torch.round(lat).to(torch.int32).view(2, 96, 60))
+    back = K.symbols_to_latent(sym.to(dev), 6, 10, 96).cpu()
+    assert torch.equal(from_nhwc(back, 96), torch.round(lat))
+    sigma = torch.exp(torch.randn(2, 96, 6, 10, generator=g) * 2)
+    table = EM.get_scale_table()
+    idx = K.build_indexes(to_nhwc(sigma).to(dev), table.to(dev), 96).cpu().numpy()
+    ref = R.build_indexes(sigma.numpy(), table.numpy()).reshape(2, 96, 60)
+    assert (idx == ref).all()
+
+
+def _rand_streams(S, n, ntab, rng, escapes=True):
+    sym = np.round(rng.laplace(0, 3, (S, n))).astype(np.int32)
+    if escapes:
+        k = max(1, S * n // 50)
+        sym.flat[rng.integers(0, S * n, k)] = rng.integers(-70000, 70000, k)
+    idx = rng.integers(0, ntab, (S, n)).astype(np.int32)
+    return sym, idx
+
+
+def test_rans_device_vs_oracle(dev):
+    rng = np.random.default_rng(11)
+    lt = EM.LaplaceTables()
+    coder = EM.RangeCoder(lt.cdf, lt.cdf_length, lt.offset, dev)
+    for S, n in [(1, 1), (3, 257), (37, 500)]:
+        sym, idx = _rand_streams(S, n, 64, rng)
+        enc = coder.encode(torch.from_numpy(sym).to(dev), torch.from_numpy(idx).to(dev))
+        strings = enc.to_bytes_list()
+        for s in range(S):
+            assert strings[s] == R.CRef.encode(sym[s], idx[s], lt.cdf, lt.cdf_length, lt.offset)
+        dec = coder.decode(enc, torch.from_numpy(idx).to(dev)).cpu().numpy()
+        assert (dec == sym).all()
+
+
+def test_rans_compressai_api(dev):
+    rng = np.random.default_rng(12)
+    ft_prm = rng.normal(0, 0.01, (11, 8)).astype(np.float32)
+    ft = EM.FactorizedTables(ft_prm)
+    cdfs = [list(ft.cdf[i, : ft.cdf_length[i]]) for i in range(8)]
+    sym = list(np.round(rng.normal(0, 20, 300)).astype(int))
+    idx = list(rng.integers(0, 8, 300))
+    s = EM.RansEncoder(dev).encode_with_indexes(sym, idx, cdfs, list(ft.cdf_length), list(ft.offset))
+    assert s == R.rans_encode_py(sym, idx, ft.cdf, ft.cdf_length, ft.offset)
+    assert EM.RansDecoder(dev).decode_with_indexes(s, idx, cdfs, list(ft.cdf_length), list(ft.offset)) == sym

@@ -1,0 +1,69 @@
+"""CPU: the oracle (oracle/dvc_ref.py) against the golden fixtures produced by the reference
+DVC forward itself (tests/golden/gen_golden.py). Pins the oracle before it is trusted."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import dvc_ref
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+STAGES = ["estmv", "mvfeature", "quant_mv", "quant_mv_upsample", "warpframe", "prediction", "feature", "z",
+          "compressed_z", "recon_sigma", "compressed_feature", "recon_res"]
+OUTS = ["clipped", "mse_loss", "warploss", "interloss", "bpp_feature", "bpp_z", "bpp_mv", "bpp"]
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _threads():
+    n = torch.get_num_threads()
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+    yield
+    torch.set_num_threads(n)
+
+
+@pytest.mark.parametrize("size", ["64x64", "128x192", "256x256"])
+def test_oracle_matches_reference(seeded_sd, size):
+    g = np.load(os.path.join(GOLD, f"dvc_{size}.npz"))
+    out, inter = dvc_ref.forward(seeded_sd, torch.from_numpy(g["input_image"]), torch.from_numpy(g["referframe"]),
+                                 return_intermediates=True)
+    for k in STAGES:
+        exp = g[k]
+        got = inter[k].numpy()
+        assert got.shape == exp.shape, k
+        assert np.abs(got - exp).max() <= 1e-5 * (np.abs(exp).max() + 1), k
+    for k in ("quant_mv", "compressed_z", "compressed_feature"):
+        assert (inter[k].numpy() == g[k]).all(), f"{k}: symbols must match exactly"
+    for n, o in zip(OUTS, out):
+        assert np.allclose(o.numpy(), g[n], rtol=1e-6, atol=1e-7), n
+
+
+def test_oracle_gop_chain(seeded_sd):
+    g = np.load(os.path.join(GOLD, "dvc_chain_256x256.npz"))
+    gop = torch.from_numpy(g["gop"])
+    x_prev = gop[0:1]
+    for i in range(1, 4):
+        out = dvc_ref.forward(seeded_sd, gop[i:i + 1], x_prev)
+        assert abs(float(out[7]) - float(g[f"f{i}_bpp"])) <= 1e-6 * abs(float(g[f"f{i}_bpp"]))
+        assert abs(float(out[1]) - float(g[f"f{i}_mse_loss"])) <= 1e-6 * float(g[f"f{i}_mse_loss"])
+        assert np.abs(out[0].numpy() - g[f"f{i}_clipped"]).max() <= 1e-5
+        x_prev = out[0]
+
+
+def test_oracle_decode_reproduces_encoder(seeded_sd):
+    """Decoder-side reconstruction from the three latents == the encoder's clipped recon."""
+    g = np.load(os.path.join(GOLD, "dvc_64x64.npz"))
+    rec, sigma = dvc_ref.decode(seeded_sd, torch.from_numpy(g["referframe"]), torch.from_numpy(g["quant_mv"]),
+                                torch.from_numpy(g["compressed_z"]), torch.from_numpy(g["compressed_feature"]))
+    assert np.abs(rec.numpy() - g["clipped"]).max() <= 1e-6
+    assert np.abs(sigma.numpy() - g["recon_sigma"]).max() <= 1e-5 * np.abs(g["recon_sigma"]).max()
+
+
+def test_warp_closed_form_edges():
+    """Appendix B.1 properties: zero flow is the align-corners/half-pixel quirk, border clamps."""
+    im = torch.arange(2 * 3 * 5 * 7, dtype=torch.float32).view(2, 3, 5, 7)
+    w0 = dvc_ref.warp(im, torch.zeros(2, 2, 5, 7))
+    # zero flow samples x = j*W/(W-1) - 0.5: corners map exactly, interior is a tiny blend
+    assert torch.allclose(w0[..., 0, 0], im[..., 0, 0]) and torch.allclose(w0[..., -1, -1], im[..., -1, -1])
+    big = dvc_ref.warp(im, torch.full((2, 2, 5, 7), 1000.0))
+    assert torch.allclose(big, im[..., -1:, -1:].expand_as(big))
