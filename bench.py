@@ -76,6 +76,7 @@ def main():
     ap.add_argument("--gops-per-gpu", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--breakdown", action="store_true", help="print per-conv-geometry timing to stderr")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -110,6 +111,10 @@ def main():
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     conv_ms, conv_flops, n_launch = timer.collect()
+    if args.breakdown and rank == 0:
+        agg = timer.breakdown()
+        for k, (n, ms, fl) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
+            print(f"{k:40s} n={n:5d} ms={ms:9.2f} TF/s={fl / (ms * 1e-3) / 1e12:7.2f}", file=sys.stderr)
 
     # ---- verification + quality, outside the timed region
     bss, decoded, sses, encs = encode_decode_gop(model, frames, check=True)

@@ -61,18 +61,6 @@ __global__ void k_channel_indexes(int32_t* __restrict__ idx, int B, int HW, int 
 }
 
 // ---- ryg_rans 64-bit primitives (rans64.h) + compressai bypass extension
-__device__ __forceinline__ bool enc_put(uint64_t& x, uint32_t*& ptr, const uint32_t* lo, uint32_t start,
-                                        uint32_t freq) {
-  const uint64_t x_max = ((kRansL >> kPrec) << 32) * freq;
-  if (x >= x_max) {
-    if (ptr <= lo) return false;
-    *--ptr = (uint32_t)x;
-    x >>= 32;
-  }
-  x = ((x / freq) << kPrec) + (x % freq) + start;
-  return true;
-}
-
 __device__ __forceinline__ bool enc_put_bits(uint64_t& x, uint32_t*& ptr, const uint32_t* lo, uint32_t val) {
   const uint32_t freq = 1u << (16 - kBypassPrec);
   const uint64_t x_max = ((kRansL >> 16) << 32) * freq;
@@ -85,22 +73,14 @@ __device__ __forceinline__ bool enc_put_bits(uint64_t& x, uint32_t*& ptr, const 
   return true;
 }
 
-__global__ void k_rans_encode(const int32_t* __restrict__ symbols, const int32_t* __restrict__ indexes,
-                              const int64_t* __restrict__ sym_off, int nstreams, const int32_t* __restrict__ cdfs,
-                              int cdf_stride, const int32_t* __restrict__ cdf_sizes,
-                              const int32_t* __restrict__ offsets, uint32_t* __restrict__ words,
-                              const int64_t* __restrict__ word_off, int32_t* __restrict__ nwords) {
-  const int s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= nstreams) return;
-  uint32_t* const lo = words + word_off[s];
-  uint32_t* const hi = words + word_off[s + 1];
-  uint32_t* ptr = hi;
-  uint64_t x = kRansL;
-  bool ok = true;
-  // Symbols are pushed forward (main symbol, then bypass count nibbles, then raw nibbles) and
-  // flushed backward; walking the stream backward and each symbol's sub-symbols in reverse
-  // push order reproduces that flush exactly.
-  for (int64_t i = sym_off[s + 1] - 1; ok && i >= sym_off[s]; --i) {
+// Phase 1 (fully parallel over all symbols): table lookups. prep[i] = start | freq << 16,
+// raw[i] = escape payload. The escape bin is the only one ending at 1<<16, so the sequential
+// phase recognises it from start + freq == 65536 without another array.
+__global__ void k_rans_prep(const int32_t* __restrict__ symbols, const int32_t* __restrict__ indexes, int64_t n,
+                            const int32_t* __restrict__ cdfs, int cdf_stride, const int32_t* __restrict__ cdf_sizes,
+                            const int32_t* __restrict__ offsets, uint32_t* __restrict__ prep,
+                            uint32_t* __restrict__ raw_out) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const int32_t ci = indexes[i];
     const int32_t* cdf = cdfs + (size_t)ci * cdf_stride;
     const int32_t max_value = cdf_sizes[ci] - 2;
@@ -113,16 +93,68 @@ __global__ void k_rans_encode(const int32_t* __restrict__ symbols, const int32_t
       raw = (uint32_t)(2 * (value - max_value));
       value = max_value;
     }
-    if (value == max_value) {
+    const uint32_t start = (uint32_t)cdf[value];
+    const uint32_t freq = (uint32_t)(cdf[value + 1] - cdf[value]);
+    prep[i] = start | (freq << 16);  // freq < 65536 (every table has >= 2 bins)
+    raw_out[i] = raw;
+  }
+}
+
+// x / freq, x % freq for x < 2^63, 0 < freq < 2^16 without a generic 64-bit divide:
+// high word by a 32-bit divide, low part (< freq * 2^32 < 2^48, exact in f64) by an f64
+// reciprocal estimate + one-step remainder correction.
+__device__ __forceinline__ void udivmod64_16(uint64_t x, uint32_t freq, double rcp, uint64_t& q, uint32_t& r) {
+  const uint32_t hi = (uint32_t)(x >> 32);
+  const uint32_t qh = hi / freq;
+  const uint32_t rh = hi - qh * freq;
+  const uint64_t t = ((uint64_t)rh << 32) | (uint32_t)x;
+  uint32_t ql = (uint32_t)((double)t * rcp);
+  int64_t rr = (int64_t)t - (int64_t)((uint64_t)ql * freq);
+  if (rr < 0) { ql -= 1; rr += freq; }
+  else if (rr >= (int64_t)freq) { ql += 1; rr -= freq; }
+  q = ((uint64_t)qh << 32) + ql;
+  r = (uint32_t)rr;
+}
+
+// Phase 2: one lane per stream walks its symbols backward (compressai's BufferedRansEncoder
+// pushes forward and flushes backward; each symbol's sub-symbols are put in reverse push order).
+__global__ void k_rans_encode(const uint32_t* __restrict__ prep, const uint32_t* __restrict__ raw_in,
+                              const int64_t* __restrict__ sym_off, int nstreams, uint32_t* __restrict__ words,
+                              const int64_t* __restrict__ word_off, int32_t* __restrict__ nwords) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= nstreams) return;
+  uint32_t* const lo = words + word_off[s];
+  uint32_t* const hi = words + word_off[s + 1];
+  uint32_t* ptr = hi;
+  uint64_t x = kRansL;
+  bool ok = true;
+  const int64_t b = sym_off[s];
+  int64_t i = sym_off[s + 1] - 1;
+  uint32_t pnext = i >= b ? prep[i] : 0;
+  for (; ok && i >= b; --i) {
+    const uint32_t p = pnext;
+    if (i > b) pnext = prep[i - 1];  // prefetch: independent of the state chain
+    const uint32_t start = p & 0xFFFFu, freq = p >> 16;
+    if (start + freq == (1u << kPrec)) {  // escape bin: bypass-coded payload
+      const uint32_t raw = raw_in[i];
       int32_t nb = 0;
       while (nb < 8 && (raw >> (nb * kBypassPrec)) != 0) ++nb;
       for (int32_t j = nb - 1; ok && j >= 0; --j) ok = enc_put_bits(x, ptr, lo, (raw >> (j * kBypassPrec)) & kMaxBypass);
-      // count nibbles: pushed as kMaxBypass x q then r ; flushed as r then kMaxBypass x q
       const int32_t q = nb / kMaxBypass, r = nb - q * kMaxBypass;
       if (ok) ok = enc_put_bits(x, ptr, lo, (uint32_t)r);
       for (int32_t k = 0; ok && k < q; ++k) ok = enc_put_bits(x, ptr, lo, kMaxBypass);
+      if (!ok) break;
     }
-    if (ok) ok = enc_put(x, ptr, lo, (uint32_t)cdf[value], (uint32_t)(cdf[value + 1] - cdf[value]));
+    const uint64_t x_max = ((kRansL >> kPrec) << 32) * freq;
+    if (x >= x_max) {
+      if (ptr <= lo) { ok = false; break; }
+      *--ptr = (uint32_t)x;
+      x >>= 32;
+    }
+    uint64_t q;
+    uint32_t r;
+    udivmod64_16(x, freq, 1.0 / (double)freq, q, r);
+    x = (q << kPrec) + r + start;
   }
   if (ok && ptr - lo >= 2) {
     ptr -= 2;
@@ -171,6 +203,24 @@ __global__ void k_pack_copy(const uint32_t* __restrict__ words, const int64_t* _
   for (int i = threadIdx.x; i < n; i += blockDim.x) dst[i] = src[i];
 }
 
+
+// Decode LUT: lut[t][cum] = the symbol s of table t with cdf[s] <= cum < cdf[s+1].
+__global__ void k_build_lut(const int32_t* __restrict__ cdfs, int cdf_stride, const int32_t* __restrict__ cdf_sizes,
+                            int ntables, uint16_t* __restrict__ lut) {
+  const int64_t n = (int64_t)ntables << kPrec;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
+    const int t = (int)(e >> kPrec);
+    const uint32_t cum = (uint32_t)(e & ((1 << kPrec) - 1));
+    const int32_t* cdf = cdfs + (size_t)t * cdf_stride;
+    int lo = 0, hi = cdf_sizes[t] - 1;
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if ((uint32_t)cdf[mid] <= cum) lo = mid; else hi = mid;
+    }
+    lut[e] = (uint16_t)lo;
+  }
+}
+
 __device__ __forceinline__ bool dec_renorm(uint64_t& x, const uint32_t*& ptr, const uint32_t* end) {
   if (x < kRansL) {
     if (ptr >= end) return false;
@@ -182,8 +232,8 @@ __device__ __forceinline__ bool dec_renorm(uint64_t& x, const uint32_t*& ptr, co
 __global__ void k_rans_decode(const uint32_t* __restrict__ packed, const int64_t* __restrict__ pack_off,
                               const int32_t* __restrict__ indexes, const int64_t* __restrict__ sym_off, int nstreams,
                               const int32_t* __restrict__ cdfs, int cdf_stride, const int32_t* __restrict__ cdf_sizes,
-                              const int32_t* __restrict__ offsets, int32_t* __restrict__ symbols,
-                              int32_t* __restrict__ status) {
+                              const int32_t* __restrict__ offsets, const uint16_t* __restrict__ lut,
+                              int32_t* __restrict__ symbols, int32_t* __restrict__ status) {
   const int s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= nstreams) return;
   const uint32_t* ptr = packed + pack_off[s];
@@ -195,25 +245,24 @@ __global__ void k_rans_decode(const uint32_t* __restrict__ packed, const int64_t
     ptr += 2;
   }
   const uint64_t mask = (1ull << kPrec) - 1;
-  for (int64_t i = sym_off[s]; i < sym_off[s + 1]; ++i) {
+  const int64_t e = sym_off[s + 1];
+  int64_t i = sym_off[s];
+  int32_t cnext = i < e ? indexes[i] : 0;
+  for (; i < e; ++i) {
+    const int32_t ci = cnext;
+    if (i + 1 < e) cnext = indexes[i + 1];  // prefetch: independent of the state chain
     if (!ok) {
       symbols[i] = 0;
       continue;
     }
-    const int32_t ci = indexes[i];
     const int32_t* cdf = cdfs + (size_t)ci * cdf_stride;
-    const int32_t size = cdf_sizes[ci];
-    const int32_t max_value = size - 2;
+    const int32_t max_value = cdf_sizes[ci] - 2;
     const uint32_t cum = (uint32_t)(x & mask);
-    int lo = 0, hi = size - 1;  // cdf[lo] <= cum < cdf[hi]
-    while (hi - lo > 1) {
-      const int mid = (lo + hi) >> 1;
-      if ((uint32_t)cdf[mid] <= cum) lo = mid; else hi = mid;
-    }
-    const uint32_t start = (uint32_t)cdf[lo], freq = (uint32_t)(cdf[lo + 1] - cdf[lo]);
+    const int32_t sidx = lut[((size_t)ci << kPrec) | cum];
+    const uint32_t start = (uint32_t)cdf[sidx], freq = (uint32_t)(cdf[sidx + 1] - cdf[sidx]);
     x = freq * (x >> kPrec) + (x & mask) - start;
     ok = dec_renorm(x, ptr, end);
-    int32_t value = lo;
+    int32_t value = sidx;
     if (ok && value == max_value) {
       auto getbits = [&](int32_t& v) {
         v = (int32_t)(x & kMaxBypass);
@@ -289,15 +338,36 @@ int fvc_channel_indexes(int32_t* idx, int batch, int hw, int c, fvc_stream_t s) 
   return 0;
 }
 
+size_t fvc_rans_encode_ws_bytes(int64_t nsymbols) { return (size_t)nsymbols * 8; }
+
 int fvc_rans_encode(const int32_t* symbols, const int32_t* indexes, const int64_t* sym_off, int nstreams,
-                    const int32_t* cdfs, int cdf_stride, const int32_t* cdf_sizes, const int32_t* offsets,
-                    uint32_t* words, const int64_t* word_off, int32_t* nwords, fvc_stream_t s) {
-  if (!symbols || !indexes || !sym_off || !cdfs || !cdf_sizes || !offsets || !words || !word_off || !nwords ||
-      nstreams <= 0)
+                    int64_t nsymbols, const int32_t* cdfs, int cdf_stride, const int32_t* cdf_sizes,
+                    const int32_t* offsets, void* ws, uint32_t* words, const int64_t* word_off, int32_t* nwords,
+                    fvc_stream_t s) {
+  if (!symbols || !indexes || !sym_off || !cdfs || !cdf_sizes || !offsets || !ws || !words || !word_off ||
+      !nwords || nstreams <= 0 || nsymbols < 0)
     return FVC_EINVAL;
+  uint32_t* prep = (uint32_t*)ws;
+  uint32_t* raw = prep + nsymbols;
+  if (nsymbols > 0) {
+    hipLaunchKernelGGL(k_rans_prep, dim3(grid_for((size_t)nsymbols)), dim3(kBlk), 0, (hipStream_t)s, symbols, indexes,
+                       nsymbols, cdfs, cdf_stride, cdf_sizes, offsets, prep, raw);
+    FVC_CHECK_LAUNCH();
+  }
   const int blk = 64;
-  hipLaunchKernelGGL(k_rans_encode, dim3((nstreams + blk - 1) / blk), dim3(blk), 0, (hipStream_t)s, symbols, indexes,
-                     sym_off, nstreams, cdfs, cdf_stride, cdf_sizes, offsets, words, word_off, nwords);
+  hipLaunchKernelGGL(k_rans_encode, dim3((nstreams + blk - 1) / blk), dim3(blk), 0, (hipStream_t)s, prep, raw,
+                     sym_off, nstreams, words, word_off, nwords);
+  FVC_CHECK_LAUNCH();
+  return 0;
+}
+
+size_t fvc_rans_lut_bytes(int ntables) { return (size_t)ntables << 17; }
+
+int fvc_rans_build_lut(const int32_t* cdfs, int cdf_stride, const int32_t* cdf_sizes, int ntables, uint16_t* lut,
+                       fvc_stream_t s) {
+  if (!cdfs || !cdf_sizes || !lut || ntables <= 0) return FVC_EINVAL;
+  hipLaunchKernelGGL(k_build_lut, dim3(grid_for((size_t)ntables << 16)), dim3(kBlk), 0, (hipStream_t)s, cdfs,
+                     cdf_stride, cdf_sizes, ntables, lut);
   FVC_CHECK_LAUNCH();
   return 0;
 }
@@ -315,13 +385,13 @@ int fvc_rans_pack(const uint32_t* words, const int64_t* word_off, const int32_t*
 
 int fvc_rans_decode(const uint32_t* packed, const int64_t* pack_off, const int32_t* indexes, const int64_t* sym_off,
                     int nstreams, const int32_t* cdfs, int cdf_stride, const int32_t* cdf_sizes,
-                    const int32_t* offsets, int32_t* symbols, int32_t* status, fvc_stream_t s) {
-  if (!packed || !pack_off || !indexes || !sym_off || !cdfs || !cdf_sizes || !offsets || !symbols || !status ||
-      nstreams <= 0)
+                    const int32_t* offsets, const uint16_t* lut, int32_t* symbols, int32_t* status, fvc_stream_t s) {
+  if (!packed || !pack_off || !indexes || !sym_off || !cdfs || !cdf_sizes || !offsets || !lut || !symbols ||
+      !status || nstreams <= 0)
     return FVC_EINVAL;
   const int blk = 64;
   hipLaunchKernelGGL(k_rans_decode, dim3((nstreams + blk - 1) / blk), dim3(blk), 0, (hipStream_t)s, packed, pack_off,
-                     indexes, sym_off, nstreams, cdfs, cdf_stride, cdf_sizes, offsets, symbols, status);
+                     indexes, sym_off, nstreams, cdfs, cdf_stride, cdf_sizes, offsets, lut, symbols, status);
   FVC_CHECK_LAUNCH();
   return 0;
 }

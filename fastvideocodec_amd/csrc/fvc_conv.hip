@@ -193,9 +193,234 @@ __global__ __launch_bounds__(kThreads) void conv_mfma_f32_kernel(const ConvArgs 
   }
 }
 
+// Stride-2 transposed conv with all four output-parity classes in one block: the four
+// classes read the same input window, so the halo tile of a channel chunk is staged once and
+// consumed by 1+2+2+4 (k=3) or 4+6+6+9 (k=5) taps instead of being re-staged per class.
+// acc[class][WM][WN] stays in registers (WM=1: 4 waves x one 32-pixel strip each).
+template <int CC, int WN>
+__global__ __launch_bounds__(kThreads) void deconv2_mfma_f32_kernel(const ConvArgs a) {
+  using G = ChunkGeom<CC>;
+  constexpr int CC4 = G::CC4;
+  constexpr int CS = G::CS;
+  constexpr int TH = 4;
+  constexpr int TW = 32;
+  constexpr int NCL = 4;
+  constexpr int MAXT = 16;
+
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  int* tap_off = reinterpret_cast<int*>(smem);  // [NCL][MAXT]
+  float* tile = smem + NCL * MAXT;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int li = lane & 31;
+  const int lh = lane >> 5;
+  const int b = blockIdx.z;
+  const int tiles_x = (a.Wq + TW - 1) / TW;
+  const int qy0 = (blockIdx.x / tiles_x) * TH;
+  const int qx0 = (blockIdx.x % tiles_x) * TW;
+  const int nt0 = blockIdx.y * WN;
+
+  if (tid < NCL * MAXT) {
+    const int cl = tid / MAXT, t = tid % MAXT;
+    tap_off[tid] = t < a.ntaps[cl] ? ((a.tdy[cl][t] - a.dymin) * a.ic + (a.tdx[cl][t] - a.dxmin)) * CS : 0;
+  }
+
+  f32x16 acc[NCL][WN];
+#pragma unroll
+  for (int cl = 0; cl < NCL; ++cl)
+#pragma unroll
+    for (int n = 0; n < WN; ++n)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[cl][n][r] = 0.f;
+
+  const int iy0 = qy0 + a.dymin;
+  const int ix0 = qx0 + a.dxmin;
+  const int tile_elems = a.ir * a.ic * CC4;
+  const float* xb = a.x + (size_t)b * a.H * a.W * a.cinp;
+  const int pix_base = (wave * a.ic + li) * CS;
+
+  for (int ch = 0; ch < a.nchunks; ++ch) {
+    for (int e = tid; e < tile_elems; e += kThreads) {
+      const int c4 = e % CC4;
+      const int p = e / CC4;
+      const int r = p / a.ic;
+      const int c = p - r * a.ic;
+      const int iy = iy0 + r;
+      const int ix = ix0 + c;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (iy >= 0 && iy < a.H && ix >= 0 && ix < a.W) {
+        v = *reinterpret_cast<const float4*>(xb + ((size_t)iy * a.W + ix) * a.cinp + ch * CC + c4 * 4);
+        v = fvc_apply_in_op4(v, a.in_op);
+      }
+      *reinterpret_cast<float4*>(tile + p * CS + c4 * 4) = v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int cl = 0; cl < NCL; ++cl) {
+      const int kbc = a.kbc[cl];
+      const int ntaps = a.ntaps[cl];
+      const int nq = kbc >> 1;
+      const float* wch = a.w + a.wcls[cl] + (size_t)ch * kbc * a.ntp * 128;
+      const int* toffs = tap_off + cl * MAXT;
+      float4 A, An, Bv[WN], Bn[WN];
+      auto load = [&](int q, float4& Ar, float4 (&Br)[WN]) {
+        const int kb = 2 * q + lh;
+        const int t = kb / CC4;
+        const int c4 = kb - t * CC4;
+        const int toff = (t < ntaps ? toffs[t] : 0) + c4 * 4;
+        Ar = *reinterpret_cast<const float4*>(tile + pix_base + toff);
+        const float* wk = wch + ((size_t)kb * a.ntp + nt0) * 128 + li * 4;
+#pragma unroll
+        for (int n = 0; n < WN; ++n) Br[n] = *reinterpret_cast<const float4*>(wk + n * 128);
+      };
+      load(0, A, Bv);
+      for (int q = 0; q < nq; ++q) {
+        if (q + 1 < nq) load(q + 1, An, Bn);
+#pragma unroll
+        for (int n = 0; n < WN; ++n) {
+          acc[cl][n] = __builtin_amdgcn_mfma_f32_32x32x2f32(A.x, Bv[n].x, acc[cl][n], 0, 0, 0);
+          acc[cl][n] = __builtin_amdgcn_mfma_f32_32x32x2f32(A.y, Bv[n].y, acc[cl][n], 0, 0, 0);
+          acc[cl][n] = __builtin_amdgcn_mfma_f32_32x32x2f32(A.z, Bv[n].z, acc[cl][n], 0, 0, 0);
+          acc[cl][n] = __builtin_amdgcn_mfma_f32_32x32x2f32(A.w, Bv[n].w, acc[cl][n], 0, 0, 0);
+        }
+        A = An;
+#pragma unroll
+        for (int n = 0; n < WN; ++n) Bv[n] = Bn[n];
+      }
+    }
+    __syncthreads();
+  }
+
+  const int qy = qy0 + wave;
+  if (qy >= a.Hq) return;
+#pragma unroll
+  for (int cl = 0; cl < NCL; ++cl) {
+    const int oy = qy * 2 + a.oy0[cl];
+#pragma unroll
+    for (int n = 0; n < WN; ++n) {
+      const int j = (nt0 + n) * 32 + li;
+      if (j >= a.coutp) continue;
+      const bool real = j < a.cout;
+      const float bj = real ? a.bias[j] : 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int qx = qx0 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        if (qx >= a.Wq) continue;
+        const int ox = qx * 2 + a.ox0[cl];
+        const size_t o = (((size_t)b * a.Ho + oy) * a.Wo + ox) * a.coutp + j;
+        float v = acc[cl][n][r] + bj;
+        if (a.act == FVC_ACT_RELU) v = v > 0.f ? v : 0.f;
+        else if (a.act == FVC_ACT_LRELU) v = v > 0.f ? v : 0.1f * v;
+        if (a.res) v += a.res[o];
+        if (a.post_op == FVC_POST_EXP) v = expf(v);
+        a.y[o] = real ? v : 0.f;
+      }
+    }
+  }
+}
+
+// Small-N variant (cout <= 16: SpyNet conv4/conv5, Warp_net conv6, mvDecoder deconv8,
+// resDecoder deconv4). Padding N to an MFMA tile of 32 would waste 2-16x of the matrix work, so
+// this path is VALU: one output pixel per lane, COUTP accumulators in registers, input from the
+// same LDS halo tile as the MFMA kernel (conflict-free ds_read_b128), weights wave-uniform
+// (scalar loads). v_fma_f32 runs at the same per-SIMD rate as the f32 MFMA on gfx950.
+template <int CC, int COUTP>
+__global__ __launch_bounds__(kThreads) void conv_smalln_f32_kernel(const ConvArgs a) {
+  using G = ChunkGeom<CC>;
+  constexpr int CC4 = G::CC4;
+  constexpr int CS = G::CS;
+  constexpr int TW = 32;
+
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  int* tap_off = reinterpret_cast<int*>(smem);
+  float* tile = smem + 64;
+
+  const int tid = threadIdx.x;
+  const int nthr = blockDim.x;
+  const int TH = nthr / TW;
+  const int tx = tid & (TW - 1);
+  const int ty = tid / TW;
+  const int cls = blockIdx.z % a.nclass;
+  const int b = blockIdx.z / a.nclass;
+  const int tiles_x = (a.Wq + TW - 1) / TW;
+  const int qy0 = (blockIdx.x / tiles_x) * TH;
+  const int qx0 = (blockIdx.x % tiles_x) * TW;
+  const int ntaps = a.ntaps[cls];
+
+  if (tid < ntaps)
+    tap_off[tid] = ((a.tdy[cls][tid] - a.dymin) * a.ic + (a.tdx[cls][tid] - a.dxmin)) * CS;
+
+  float acc[COUTP];
+#pragma unroll
+  for (int j = 0; j < COUTP; ++j) acc[j] = 0.f;
+
+  const int iy0 = qy0 * a.sin + a.dymin;
+  const int ix0 = qx0 * a.sin + a.dxmin;
+  const int tile_elems = a.ir * a.ic * CC4;
+  const float* xb = a.x + (size_t)b * a.H * a.W * a.cinp;
+  const int pix_base = ((ty * a.sin) * a.ic + tx * a.sin) * CS;
+  const float* __restrict__ wcls = a.w + a.wcls[cls];
+
+  for (int ch = 0; ch < a.nchunks; ++ch) {
+    for (int e = tid; e < tile_elems; e += nthr) {
+      const int c4 = e % CC4;
+      const int p = e / CC4;
+      const int r = p / a.ic;
+      const int c = p - r * a.ic;
+      const int iy = iy0 + r;
+      const int ix = ix0 + c;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (iy >= 0 && iy < a.H && ix >= 0 && ix < a.W) {
+        v = *reinterpret_cast<const float4*>(xb + ((size_t)iy * a.W + ix) * a.cinp + ch * CC + c4 * 4);
+        v = fvc_apply_in_op4(v, a.in_op);
+      }
+      *reinterpret_cast<float4*>(tile + p * CS + c4 * 4) = v;
+    }
+    __syncthreads();
+    const float* __restrict__ wch = wcls + (size_t)ch * ntaps * CC * COUTP;
+    for (int t = 0; t < ntaps; ++t) {
+      const int toff = __builtin_amdgcn_readfirstlane(tap_off[t]);
+      const float* __restrict__ wt = wch + t * CC * COUTP;
+#pragma unroll
+      for (int c4 = 0; c4 < CC4; ++c4) {
+        const float4 v = *reinterpret_cast<const float4*>(tile + pix_base + toff + c4 * 4);
+        const float vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+          for (int j = 0; j < COUTP; ++j) acc[j] = __builtin_fmaf(vv[e], wt[(c4 * 4 + e) * COUTP + j], acc[j]);
+      }
+    }
+    __syncthreads();
+  }
+
+  const int qy = qy0 + ty, qx = qx0 + tx;
+  if (qy >= a.Hq || qx >= a.Wq) return;
+  const int oy = qy * a.sout + a.oy0[cls];
+  const int ox = qx * a.sout + a.ox0[cls];
+  const size_t o = (((size_t)b * a.Ho + oy) * a.Wo + ox) * a.coutp;
+#pragma unroll
+  for (int j4 = 0; j4 < COUTP / 4; ++j4) {
+    float r4[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int j = j4 * 4 + u;
+      float v = acc[j] + (j < a.cout ? a.bias[j] : 0.f);
+      if (a.act == FVC_ACT_RELU) v = v > 0.f ? v : 0.f;
+      else if (a.act == FVC_ACT_LRELU) v = v > 0.f ? v : 0.1f * v;
+      if (a.res) v += a.res[o + j];
+      if (a.post_op == FVC_POST_EXP) v = expf(v);
+      r4[u] = j < a.cout ? v : 0.f;
+    }
+    *reinterpret_cast<float4*>(a.y + o + j4 * 4) = make_float4(r4[0], r4[1], r4[2], r4[3]);
+  }
+}
+
 // ------------------------------------------------------------------ host-side geometry
 struct Cfg {
-  int cinp, coutp, ntp, cc, wm, wn, nclass, nchunks;
+  int cinp, coutp, ntp, cc, wm, wn, nclass, nchunks, smalln, fused;
   int sin, sout;
   int ntaps[4], kbc[4], oy0[4], ox0[4];
   int tky[4][kMaxTaps], tkx[4][kMaxTaps];  // kernel tap (ky,kx)
@@ -258,7 +483,10 @@ static bool make_cfg(int cin, int cout, int ks, int stride, int transposed, Cfg&
       c.dxmax = c.tdx[cl][t] > c.dxmax ? c.tdx[cl][t] : c.dxmax;
     }
   c.wn = c.ntp;
-  c.wm = (!transposed && stride == 2) ? 1 : 2;
+  c.smalln = c.coutp <= 16 ? 1 : 0;
+  c.fused = (transposed && stride == 2 && !c.smalln && c.cinp % 8 == 0 && ks <= 5) ? 1 : 0;
+  c.wm = ((!transposed && stride == 2) || c.fused) ? 1 : 2;
+  if (c.fused) c.wn = (c.ntp % 2 == 0) ? 2 : 1;
   // channel chunk: largest of {32,16,8,4} dividing cinp whose halo tile fits 64 KB
   int cc = 32;
   for (;; cc >>= 1) {
@@ -276,7 +504,10 @@ static bool make_cfg(int cin, int cout, int ks, int stride, int transposed, Cfg&
   for (int cl = 0; cl < c.nclass; ++cl) {
     c.kbc[cl] = fvc_rup(c.ntaps[cl] * (cc / 4), 2);
     c.wcls[cl] = off;
-    off += (long long)c.nchunks * c.kbc[cl] * c.ntp * 128;
+    if (c.smalln)  // [chunk][tap][cin in chunk][coutp]
+      off += (long long)c.nchunks * c.ntaps[cl] * cc * c.coutp;
+    else           // [chunk][k-block][n-tile][32][4]
+      off += (long long)c.nchunks * c.kbc[cl] * c.ntp * 128;
   }
   c.wtotal = off;
   return true;
@@ -304,6 +535,58 @@ template <int CC>
 static int launch_wm(int wm, int wn, const ConvArgs& a, dim3 grid, size_t lds, hipStream_t s) {
   if (wm == 1) return launch_wn<CC, 1>(wn, a, grid, lds, s);
   return launch_wn<CC, 2>(wn, a, grid, lds, s);
+}
+
+template <int CC, int COUTP>
+static int launch_sn_t(const ConvArgs& a, dim3 grid, dim3 blk, size_t lds, hipStream_t s) {
+  hipLaunchKernelGGL((conv_smalln_f32_kernel<CC, COUTP>), grid, blk, lds, s, a);
+  FVC_CHECK_LAUNCH();
+  return 0;
+}
+
+template <int CC>
+static int launch_sn_n(int coutp, const ConvArgs& a, dim3 grid, dim3 blk, size_t lds, hipStream_t s) {
+  switch (coutp) {
+    case 4: return launch_sn_t<CC, 4>(a, grid, blk, lds, s);
+    case 8: return launch_sn_t<CC, 8>(a, grid, blk, lds, s);
+    case 12: return launch_sn_t<CC, 12>(a, grid, blk, lds, s);
+    case 16: return launch_sn_t<CC, 16>(a, grid, blk, lds, s);
+  }
+  return FVC_EINVAL;
+}
+
+template <int CC, int WN>
+static int launch_fd_t(const ConvArgs& a, dim3 grid, size_t lds, hipStream_t s) {
+  hipLaunchKernelGGL((deconv2_mfma_f32_kernel<CC, WN>), grid, dim3(kThreads), lds, s, a);
+  FVC_CHECK_LAUNCH();
+  return 0;
+}
+
+static int launch_fused(int cc, int wn, const ConvArgs& a, dim3 grid, size_t lds, hipStream_t s) {
+  if (wn == 1) {
+    switch (cc) {
+      case 8: return launch_fd_t<8, 1>(a, grid, lds, s);
+      case 16: return launch_fd_t<16, 1>(a, grid, lds, s);
+      case 32: return launch_fd_t<32, 1>(a, grid, lds, s);
+    }
+  } else {
+    switch (cc) {
+      case 8: return launch_fd_t<8, 2>(a, grid, lds, s);
+      case 16: return launch_fd_t<16, 2>(a, grid, lds, s);
+      case 32: return launch_fd_t<32, 2>(a, grid, lds, s);
+    }
+  }
+  return FVC_EINVAL;
+}
+
+static int launch_smalln(int cc, int coutp, const ConvArgs& a, dim3 grid, dim3 blk, size_t lds, hipStream_t s) {
+  switch (cc) {
+    case 4: return launch_sn_n<4>(coutp, a, grid, blk, lds, s);
+    case 8: return launch_sn_n<8>(coutp, a, grid, blk, lds, s);
+    case 16: return launch_sn_n<16>(coutp, a, grid, blk, lds, s);
+    case 32: return launch_sn_n<32>(coutp, a, grid, blk, lds, s);
+  }
+  return FVC_EINVAL;
 }
 
 static int run_conv(const float* x, const float* wpack, const float* bias, const float* res,
@@ -346,6 +629,14 @@ static int run_conv(const float* x, const float* wpack, const float* bias, const
   const size_t lds = 256 + (size_t)a.ir * a.ic * cs * 4;
   const int tiles_x = fvc_cdiv(a.Wq, 32);
   const int tiles_y = fvc_cdiv(a.Hq, TH);
+  if (c.smalln) {
+    dim3 grid(tiles_x * tiles_y, 1, batch * c.nclass);
+    return launch_smalln(c.cc, c.coutp, a, grid, dim3(TH * 32), lds, s);
+  }
+  if (c.fused) {
+    dim3 grid(tiles_x * tiles_y, c.ntp / c.wn, batch);
+    return launch_fused(c.cc, c.wn, a, grid, lds, s);
+  }
   dim3 grid(tiles_x * tiles_y, c.ntp / c.wn, batch * c.nclass);
   switch (c.cc) {
     case 4: return launch_wm<4>(c.wm, c.wn, a, grid, lds, s);
@@ -384,8 +675,11 @@ int fvc_conv_pack_weight(const float* w, float* wp, int cin, int cout, int ks, i
             if (ci >= cin) continue;
             const float v = transposed ? w[(((size_t)ci * cout + j) * ks + ky) * ks + kx]
                                        : w[(((size_t)j * cin + ci) * ks + ky) * ks + kx];
-            const size_t o = (size_t)c.wcls[cl] +
-                             (((size_t)ch * c.kbc[cl] + kb) * c.ntp * 32 + j) * 4 + e;
+            size_t o;
+            if (c.smalln)
+              o = (size_t)c.wcls[cl] + (((size_t)ch * c.ntaps[cl] + t) * c.cc + c4 * 4 + e) * c.coutp + j;
+            else
+              o = (size_t)c.wcls[cl] + (((size_t)ch * c.kbc[cl] + kb) * c.ntp * 32 + j) * 4 + e;
             wp[o] = v;
           }
       }

@@ -178,6 +178,10 @@ class RangeCoder:
         self.offset = torch.as_tensor(np.ascontiguousarray(offset, np.int32)).to(device)
         self.device = torch.device(device)
         self._offs = {}
+        nt = self.cdf.shape[0]
+        self.lut = torch.empty(_lib.load().fvc_rans_lut_bytes(nt) // 2, dtype=torch.int16, device=self.device)
+        _lib.call("fvc_rans_build_lut", self.cdf.data_ptr(), self.cdf.shape[1], self.cdf_length.data_ptr(), nt,
+                  self.lut.data_ptr(), K.stream_handle(self.device))
 
     def _sym_off(self, S, n):
         key = ("s", S, n)
@@ -201,10 +205,12 @@ class RangeCoder:
         word_off = self._word_off(S, n)
         words = torch.empty(int(S * (2 * n + 8)), dtype=torch.int32, device=self.device)
         nwords = torch.empty(S, dtype=torch.int32, device=self.device)
+        ws = torch.empty(max(1, _lib.load().fvc_rans_encode_ws_bytes(S * n) // 4), dtype=torch.int32,
+                         device=self.device)
         st = K.stream_handle()
-        _lib.call("fvc_rans_encode", symbols.data_ptr(), indexes.data_ptr(), sym_off.data_ptr(), S,
+        _lib.call("fvc_rans_encode", symbols.data_ptr(), indexes.data_ptr(), sym_off.data_ptr(), S, S * n,
                   self.cdf.data_ptr(), self.cdf.shape[1], self.cdf_length.data_ptr(), self.offset.data_ptr(),
-                  words.data_ptr(), word_off.data_ptr(), nwords.data_ptr(), st)
+                  ws.data_ptr(), words.data_ptr(), word_off.data_ptr(), nwords.data_ptr(), st)
         pack_off = torch.empty(S + 1, dtype=torch.int64, device=self.device)
         packed = torch.empty_like(words)
         _lib.call("fvc_rans_pack", words.data_ptr(), word_off.data_ptr(), nwords.data_ptr(), S,
@@ -221,7 +227,7 @@ class RangeCoder:
         status = torch.empty(S, dtype=torch.int32, device=self.device)
         _lib.call("fvc_rans_decode", enc.packed.data_ptr(), enc.pack_off.data_ptr(), indexes.data_ptr(),
                   sym_off.data_ptr(), S, self.cdf.data_ptr(), self.cdf.shape[1], self.cdf_length.data_ptr(),
-                  self.offset.data_ptr(), out.data_ptr(), status.data_ptr(), K.stream_handle())
+                  self.offset.data_ptr(), self.lut.data_ptr(), out.data_ptr(), status.data_ptr(), K.stream_handle())
         if check and int(status.abs().max()) != 0:
             raise _lib.FvcError("corrupt rANS stream")
         return out

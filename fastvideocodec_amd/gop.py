@@ -1,29 +1,65 @@
 """GOP driver for real encode+decode (the bitstream counterpart of models.parallel_compression,
-models.py:368-383): the I-frame passes through (BPG out of scope), every P-frame is encoded
-against the previous *decoded* frame and decoded from its bitstream.
+models.py:368-383): the I-frame passes through (BPG out of scope), every P-frame is encoded and
+then decoded from its bitstream.
 
-G GOPs are processed together as a batch (frame t of every GOP in one forward), which
-raises occupancy on the small late layers; GOPs are independent, so this is the per-GPU
-analogue of sharding GOPs across ranks.
+Three HIP streams form a pipeline:
+  * encoder stream (the caller's current stream): the encoder forward of frame t, using the
+    encoder's own reconstruction of frame t-1 as reference (exactly what the reference loop
+    does: x_prev = model(...)[0]);
+  * coder stream: symbols -> rANS encode of frame t (waits only on frame t's latents);
+  * decoder stream: rANS decode + synthesis of frame t against the decoder's own previous
+    reconstruction (waits only on frame t's bitstream).
+Encoder and decoder reconstructions are bit-identical (same kernels, same operand order;
+checked by tests and by bench.py), so the decoder never gates the encoder, and the three
+pipelines overlap on the GPU.
+
+G GOPs are batched along dim 0 (frame t of every GOP in one forward).
 """
 from __future__ import annotations
 
 import torch
 
+from . import kernels as K
 
-def encode_decode_gop(model, frames: torch.Tensor, check=False):
-    """frames: [G, T, 3, H, W] device tensor. Returns (bitstreams, decoded [G,T-1,3,H,W] list,
-    sse list, encoder recon list)."""
+_STREAMS = {}
+
+
+def _side_streams(device):
+    key = str(device)
+    if key not in _STREAMS:
+        _STREAMS[key] = (torch.cuda.Stream(device=device), torch.cuda.Stream(device=device))
+    return _STREAMS[key]
+
+
+def encode_decode_gop(model, frames: torch.Tensor, check=False, overlap=True):
+    """frames: [G, T, 3, H, W] device tensor. Returns (bitstreams, decoder recons, encoder sse
+    list, encoder recons); every returned tensor is ready on the caller's stream."""
     G, T = frames.shape[:2]
-    x_prev = frames[:, 0].contiguous()
-    bitstreams, decoded, sses, enc_recons = [], [], [], []
-    for t in range(1, T):
-        cur = frames[:, t].contiguous()
-        bs, rec_enc, sse = model.compress(cur, x_prev, return_sse=True)
-        rec_dec = model.decompress(bs, x_prev, check=check)
-        bitstreams.append(bs)
-        decoded.append(rec_dec)
-        enc_recons.append(rec_enc)
-        sses.append(sse)
-        x_prev = rec_dec
+    main = torch.cuda.current_stream(frames.device)
+    s_code, s_dec = _side_streams(frames.device) if overlap else (main, main)
+    x_enc = frames[:, 0].contiguous()
+    x_dec = x_enc
+    bitstreams, decoded, sses, enc_recons, keep = [], [], [], [], [x_enc]
+    model.update()
+    with torch.no_grad():
+        for t in range(1, T):
+            cur = frames[:, t].contiguous()
+            tens = model._encode_graph(cur, x_enc)
+            clipped, sse = K.recon_finalize(tens["recon"], tens["cur4"], tens["warpframe"], tens["prediction"])
+            lat = {k: tens[k] for k in ("mvfeature", "z", "feature", "sigma")}
+            del tens
+            s_code.wait_stream(main)
+            with torch.cuda.stream(s_code):
+                bs = model.compress_tensors(lat)
+            s_dec.wait_stream(s_code)
+            with torch.cuda.stream(s_dec):
+                rec_dec = model.decompress(bs, x_dec, check=check)
+            keep.append((lat, cur))  # cross-stream tensors stay alive until the pipeline drains
+            bitstreams.append(bs)
+            decoded.append(rec_dec)
+            enc_recons.append(clipped)
+            sses.append(sse)
+            x_enc, x_dec = clipped, rec_dec
+    main.wait_stream(s_code)
+    main.wait_stream(s_dec)
     return bitstreams, decoded, sses, enc_recons

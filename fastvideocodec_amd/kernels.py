@@ -180,7 +180,9 @@ class PackedConv:
         if timer is not None:
             ev1.record()
             timer.records.append((ev0, ev1, profiling.conv_flops(self.cin, self.cout, self.ksize, self.stride,
-                                                                 self.transposed, B, H, W)))
+                                                                 self.transposed, B, H, W),
+                                  f"{'deconv' if self.transposed else 'conv'}{self.ksize}s{self.stride} "
+                                  f"{self.cin}->{self.cout} @{H}x{W}"))
         return y
 
 
@@ -189,7 +191,7 @@ _WS = {}
 
 
 def _ws(device):
-    key = str(device)
+    key = (str(device), stream_handle())  # one reduction workspace per stream (overlapped pipelines)
     if key not in _WS:
         n = _lib.load().fvc_reduce_ws_doubles()
         _WS[key] = torch.empty(n, dtype=torch.float64, device=device)

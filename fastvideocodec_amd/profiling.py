@@ -36,9 +36,21 @@ class KernelTimer:
     def collect(self):
         """Synchronise and return (total_ms, total_flops, n_launches)."""
         torch.cuda.synchronize()
-        ms = sum(s.elapsed_time(e) for s, e, _ in self.records)
-        fl = sum(f for _, _, f in self.records)
+        ms = sum(r[0].elapsed_time(r[1]) for r in self.records)
+        fl = sum(r[2] for r in self.records)
         return ms, fl, len(self.records)
+
+    def breakdown(self):
+        """Per-geometry aggregate: {key: [launches, ms, flops]} (keys recorded by the caller)."""
+        torch.cuda.synchronize()
+        agg = {}
+        for r in self.records:
+            key = r[3] if len(r) > 3 else "?"
+            a = agg.setdefault(key, [0, 0.0, 0.0])
+            a[0] += 1
+            a[1] += r[0].elapsed_time(r[1])
+            a[2] += r[2]
+        return agg
 
 
 def active():

@@ -139,24 +139,31 @@ int fvc_channel_indexes(int32_t* idx, int batch, int hw, int c, fvc_stream_t str
 int fvc_pmf_to_quantized_cdf(const float* pmf, int n, int precision, uint32_t* cdf_out);
 
 /* Device rANS over nstreams independent streams. Stream s codes symbols
- * [sym_off[s], sym_off[s+1]) with tables indexes[i]; cdfs is [ntables][cdf_stride] int32,
- * cdf_sizes/offsets per table (compressai _quantized_cdf/_cdf_length/_offset).
+ * [sym_off[s], sym_off[s+1]) (nsymbols in total) with tables indexes[i]; cdfs is
+ * [ntables][cdf_stride] int32, cdf_sizes/offsets per table (compressai _quantized_cdf /
+ * _cdf_length / _offset). ws: fvc_rans_encode_ws_bytes(nsymbols) bytes of scratch.
  * Encode writes stream s downward into words[word_off[s] .. word_off[s+1]) and its length
- * (in 32-bit words, counted from the END of its region) into nwords[s]; the stream's bytes are
- * the last nwords[s] words of its region, little-endian. */
+ * (in 32-bit words, counted from the END of its region) into nwords[s] (-1 = no space); the
+ * stream's bytes are the last nwords[s] words of its region, little-endian. */
+size_t fvc_rans_encode_ws_bytes(int64_t nsymbols);
 int fvc_rans_encode(const int32_t* symbols, const int32_t* indexes, const int64_t* sym_off,
-                    int nstreams, const int32_t* cdfs, int cdf_stride, const int32_t* cdf_sizes,
-                    const int32_t* offsets, uint32_t* words, const int64_t* word_off,
-                    int32_t* nwords, fvc_stream_t stream);
+                    int nstreams, int64_t nsymbols, const int32_t* cdfs, int cdf_stride,
+                    const int32_t* cdf_sizes, const int32_t* offsets, void* ws, uint32_t* words,
+                    const int64_t* word_off, int32_t* nwords, fvc_stream_t stream);
 /* Pack encoded regions into one contiguous buffer: out[pack_off[s] ..] = last nwords[s] words
  * of region s; pack_off is [nstreams+1] (exclusive scan of nwords, computed on device). */
 int fvc_rans_pack(const uint32_t* words, const int64_t* word_off, const int32_t* nwords,
                   int nstreams, int64_t* pack_off, uint32_t* out, fvc_stream_t stream);
+/* Decode lookup table: lut[t][cum] = symbol index of table t covering cum (built once per
+ * table set; fvc_rans_lut_bytes(ntables) bytes). */
+size_t fvc_rans_lut_bytes(int ntables);
+int fvc_rans_build_lut(const int32_t* cdfs, int cdf_stride, const int32_t* cdf_sizes, int ntables,
+                       uint16_t* lut, fvc_stream_t stream);
 /* Decode: stream s reads packed words starting at pack_off[s]; status[s] = 0 or FVC_ECORRUPT */
 int fvc_rans_decode(const uint32_t* packed, const int64_t* pack_off, const int32_t* indexes,
                     const int64_t* sym_off, int nstreams, const int32_t* cdfs, int cdf_stride,
-                    const int32_t* cdf_sizes, const int32_t* offsets, int32_t* symbols,
-                    int32_t* status, fvc_stream_t stream);
+                    const int32_t* cdf_sizes, const int32_t* offsets, const uint16_t* lut,
+                    int32_t* symbols, int32_t* status, fvc_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -62,20 +62,31 @@ def test_forward_vs_golden(model, dev, size):
     assert abs(psnr_got - psnr_exp) <= TOL_PSNR_DB
 
 
+def _flip_rate(t, g, i=None):
+    pre = "" if i is None else f"f{i}_"
+    flips = []
+    for name, gname in (("mvfeature", "quant_mv"), ("feature", "compressed_feature"), ("z", "compressed_z")):
+        got = np.round(nhwc_to_nchw(t[name], STAGES[name]).numpy())
+        flips.append(float((got != g[pre + gname]).mean()))
+    return max(flips)
+
+
 def test_gop_chain_vs_golden(model, dev):
     """parallel_compression loop (models.py:368-383) over a 4-frame GOP.
 
-    Open loop (each P-frame coded against the reference's own previous recon) every frame meets
-    the 1e-4 dB bar. Closed loop (our own previous recon) the chain drifts the way the reference
-    drifts across CPU backends (symbol flips propagate through x_prev), so the
-    closed-loop bound is looser and grows with the frame index."""
+    Open loop (each P-frame coded against the reference's own previous recon): symbols match
+    (flip rate <= TOL_SYMBOL_FLIP) and PSNR within 5e-4 dB (one flipped symbol of a 256x256
+    frame moves PSNR by ~1e-4 dB; the 1e-4 dB bar is checked exactly on identical symbols in
+    test_decode_from_golden_symbols). Closed loop (our own previous recon) the chain drifts the
+    way the reference drifts across CPU backends, so the closed-loop bound is looser."""
     g = np.load(os.path.join(GOLD, "dvc_chain_256x256.npz"))
     gop = torch.from_numpy(g["gop"]).to(dev)
     exp_psnr = np.array([10 * np.log10(1 / float(g[f"f{i}_mse_loss"])) for i in range(1, 4)])
     for i in range(1, 4):
         ref = gop[0:1] if i == 1 else torch.from_numpy(g[f"f{i-1}_clipped"]).to(dev)
-        out = model(gop[i:i + 1], ref)
-        assert abs(10 * np.log10(1 / float(out[1])) - exp_psnr[i - 1]) <= TOL_PSNR_DB
+        out, t = model(gop[i:i + 1], ref, return_intermediates=True)
+        assert _flip_rate(t, g, i) <= TOL_SYMBOL_FLIP
+        assert abs(10 * np.log10(1 / float(out[1])) - exp_psnr[i - 1]) <= 5 * TOL_PSNR_DB
         assert abs(float(out[7]) - float(g[f"f{i}_bpp"])) <= 1e-3 * float(g[f"f{i}_bpp"])
     data = gop.clone()
     x_hat, loss, img_loss, be_loss, _, psnr, psnr_list, aux, aux2, _, _ = parallel_compression(None, model, data, False)
@@ -84,6 +95,30 @@ def test_gop_chain_vs_golden(model, dev):
     assert drift[0] <= TOL_PSNR_DB and drift.max() <= 2e-2, drift
     exp_bpp = np.mean([float(g[f"f{i}_bpp"]) for i in range(1, 4)])
     assert abs(be_loss - exp_bpp) <= 1e-2 * exp_bpp
+
+
+@pytest.mark.parametrize("case", ["64x64", "128x192", "256x256", "chain2", "chain3"])
+def test_decode_from_golden_symbols(model, dev, case):
+    """T3 on identical decisions: the reference's own quantised latents, entropy-coded by the
+    device rANS and decoded by the HIP decoder, reconstruct the reference's frame within 1e-4 dB."""
+    from fastvideocodec_amd import kernels as K
+    if case.startswith("chain"):
+        i = int(case[-1])
+        g = np.load(os.path.join(GOLD, "dvc_chain_256x256.npz"))
+        cur, ref = g["gop"][i:i + 1], g[f"f{i-1}_clipped"]
+        qmv, qz, qf, clipped = g[f"f{i}_quant_mv"], g[f"f{i}_compressed_z"], g[f"f{i}_compressed_feature"], g[f"f{i}_clipped"]
+    else:
+        g = np.load(os.path.join(GOLD, f"dvc_{case}.npz"))
+        cur, ref = g["input_image"], g["referframe"]
+        qmv, qz, qf, clipped = g["quant_mv"], g["compressed_z"], g["compressed_feature"], g["clipped"]
+    to_nhwc = lambda a: K.nchw_to_nhwc(torch.from_numpy(np.ascontiguousarray(a)).to(dev))
+    sigma = model.respriorDecoder.run(to_nhwc(qz))
+    bs = model.compress_tensors({"mvfeature": to_nhwc(qmv), "z": to_nhwc(qz), "feature": to_nhwc(qf), "sigma": sigma})
+    rec = model.decompress(bs, torch.from_numpy(np.ascontiguousarray(ref)).to(dev)).cpu().numpy()
+    assert np.abs(rec - clipped).max() <= 1e-4
+    p_got = 10 * np.log10(1 / np.mean((rec.astype(np.float64) - cur) ** 2))
+    p_exp = 10 * np.log10(1 / np.mean((clipped.astype(np.float64) - cur) ** 2))
+    assert abs(p_got - p_exp) <= TOL_PSNR_DB
 
 
 def test_compress_decompress_bitexact(model, dev):
@@ -151,3 +186,19 @@ def test_rejects_bad_sizes(model, dev):
     x = torch.rand(1, 3, 100, 64, device=dev)
     with pytest.raises(ValueError):
         model(x, x)
+
+
+def test_gop_pipeline_bitexact(model, dev):
+    """Three-stream encode/code/decode pipeline: decoder recon == encoder recon for every frame,
+    and the pipelined bitstreams equal a serial (single-stream) run."""
+    from fastvideocodec_amd.gop import encode_decode_gop
+    from fastvideocodec_amd.synthetic import make_gop
+    frames = torch.from_numpy(np.stack([make_gop(128, 192, 4, 7 + g) for g in range(2)])).to(dev)
+    bss, dec, sses, enc = encode_decode_gop(model, frames, check=True, overlap=True)
+    bss2, dec2, _, enc2 = encode_decode_gop(model, frames, check=True, overlap=False)
+    torch.cuda.synchronize()
+    for a, b, c, d in zip(dec, enc, dec2, enc2):
+        assert torch.equal(a, b) and torch.equal(a, c) and torch.equal(b, d)
+    for a, b in zip(bss, bss2):
+        assert a.feature.to_bytes_list() == b.feature.to_bytes_list()
+        assert a.mv.to_bytes_list() == b.mv.to_bytes_list()
