@@ -77,6 +77,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--breakdown", action="store_true", help="print per-conv-geometry timing to stderr")
+    ap.add_argument("--serial", action="store_true",
+                    help="one HIP stream (no encode/code/decode overlap): per-kernel durations are unshared")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -94,8 +96,9 @@ def main():
     frames = torch.from_numpy(np.stack(gops)).to(dev)  # [G, T, 3, Hp, Wp]
     Hp, Wp = frames.shape[-2:]
 
+    overlap = not args.serial
     for _ in range(args.warmup):
-        encode_decode_gop(model, frames)
+        encode_decode_gop(model, frames, overlap=overlap)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -104,7 +107,7 @@ def main():
     t0 = time.perf_counter()
     with timer:
         for _ in range(args.steps):
-            encode_decode_gop(model, frames)
+            encode_decode_gop(model, frames, overlap=overlap)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

@@ -22,6 +22,7 @@
 //    the input with a subset of taps (blockIdx.z = batch*classes + class); no zero-insertion.
 //  * epilogue: bias, activation (ReLU / LeakyReLU 0.1), residual add, exp; pad channels = 0.
 #include "fvc_common.h"
+#include <stdlib.h>
 
 namespace {
 
@@ -145,15 +146,23 @@ __global__ __launch_bounds__(kThreads) void conv_mfma_f32_kernel(const ConvArgs 
     load(0, A, Bv);
     for (int q = 0; q < nq; ++q) {
       if (q + 1 < nq) load(q + 1, An, Bn);
+      // element-major issue order: consecutive MFMAs hit different accumulators (no RAW chain)
 #pragma unroll
       for (int m = 0; m < WM; ++m)
 #pragma unroll
-        for (int n = 0; n < WN; ++n) {
-          acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x2f32(A[m].x, Bv[n].x, acc[m][n], 0, 0, 0);
-          acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x2f32(A[m].y, Bv[n].y, acc[m][n], 0, 0, 0);
-          acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x2f32(A[m].z, Bv[n].z, acc[m][n], 0, 0, 0);
-          acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x2f32(A[m].w, Bv[n].w, acc[m][n], 0, 0, 0);
-        }
+        for (int n = 0; n < WN; ++n) acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x2f32(A[m].x, Bv[n].x, acc[m][n], 0, 0, 0);
+#pragma unroll
+      for (int m = 0; m < WM; ++m)
+#pragma unroll
+        for (int n = 0; n < WN; ++n) acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x2f32(A[m].y, Bv[n].y, acc[m][n], 0, 0, 0);
+#pragma unroll
+      for (int m = 0; m < WM; ++m)
+#pragma unroll
+        for (int n = 0; n < WN; ++n) acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x2f32(A[m].z, Bv[n].z, acc[m][n], 0, 0, 0);
+#pragma unroll
+      for (int m = 0; m < WM; ++m)
+#pragma unroll
+        for (int n = 0; n < WN; ++n) acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x2f32(A[m].w, Bv[n].w, acc[m][n], 0, 0, 0);
 #pragma unroll
       for (int m = 0; m < WM; ++m) A[m] = An[m];
 #pragma unroll
@@ -179,6 +188,174 @@ __global__ __launch_bounds__(kThreads) void conv_mfma_f32_kernel(const ConvArgs 
       for (int r = 0; r < 16; ++r) {
         const int pi = (r & 3) + 8 * (r >> 2) + 4 * lh;
         const int qx = qx0 + pi;
+        if (qx >= a.Wq) continue;
+        const int ox = qx * a.sout + ox0;
+        const size_t o = (((size_t)b * a.Ho + oy) * a.Wo + ox) * a.coutp + j;
+        float v = acc[m][n][r] + bj;
+        if (a.act == FVC_ACT_RELU) v = v > 0.f ? v : 0.f;
+        else if (a.act == FVC_ACT_LRELU) v = v > 0.f ? v : 0.1f * v;
+        if (a.res) v += a.res[o];
+        if (a.post_op == FVC_POST_EXP) v = expf(v);
+        a.y[o] = real ? v : 0.f;
+      }
+    }
+  }
+}
+
+// Pipelined variant for stride-1 convs: two LDS halo-tile buffers; while the waves run the
+// MFMAs of channel chunk ch out of one buffer, each thread stages one float4 of chunk ch+1 per
+// MFMA quad into the other (global load issued before the quad's MFMAs, LDS write after), so
+// the staging latency hides under the matrix work and only one barrier per chunk remains.
+template <int CC, int WM, int WN, int NW>
+__global__ __launch_bounds__(NW * 64) void conv_mfma_pipe_kernel(const ConvArgs a) {
+  using G = ChunkGeom<CC>;
+  constexpr int CC4 = G::CC4;
+  constexpr int CS = G::CS;
+  constexpr int TH = NW * WM;
+  constexpr int TW = 32;
+  constexpr int NT = NW * 64;
+
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  int* tap_off = reinterpret_cast<int*>(smem);
+  const int tile_floats = (a.ir * a.ic * CS + 3) & ~3;
+  float* tiles[2] = {smem + 64, smem + 64 + tile_floats};
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int li = lane & 31;
+  const int lh = lane >> 5;
+  const int cls = blockIdx.z % a.nclass;
+  const int b = blockIdx.z / a.nclass;
+  const int tiles_x = (a.Wq + TW - 1) / TW;
+  const int qy0 = (blockIdx.x / tiles_x) * TH;
+  const int qx0 = (blockIdx.x % tiles_x) * TW;
+  const int nt0 = blockIdx.y * WN;
+  const int ntaps = a.ntaps[cls];
+  const int kbc = a.kbc[cls];
+  const int nq = kbc >> 1;
+
+  if (tid < ntaps) tap_off[tid] = ((a.tdy[cls][tid] - a.dymin) * a.ic + (a.tdx[cls][tid] - a.dxmin)) * CS;
+
+  const int iy0 = qy0 * a.sin + a.dymin;
+  const int ix0 = qx0 * a.sin + a.dxmin;
+  const int tile_elems = a.ir * a.ic * CC4;
+  const float* xb = a.x + (size_t)b * a.H * a.W * a.cinp;
+
+  auto fetch = [&](int e, int ch, float4& v, int& dst) {
+    const int c4 = e % CC4;
+    const int p = e / CC4;
+    const int r = p / a.ic;
+    const int c = p - r * a.ic;
+    const int iy = iy0 + r, ix = ix0 + c;
+    v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (iy >= 0 && iy < a.H && ix >= 0 && ix < a.W) {
+      v = *reinterpret_cast<const float4*>(xb + ((size_t)iy * a.W + ix) * a.cinp + ch * CC + c4 * 4);
+      v = fvc_apply_in_op4(v, a.in_op);
+    }
+    dst = p * CS + c4 * 4;
+  };
+
+  // prologue: chunk 0
+  for (int e = tid; e < tile_elems; e += NT) {
+    float4 v;
+    int d;
+    fetch(e, 0, v, d);
+    *reinterpret_cast<float4*>(tiles[0] + d) = v;
+  }
+
+  f32x16 acc[WM][WN];
+#pragma unroll
+  for (int m = 0; m < WM; ++m)
+#pragma unroll
+    for (int n = 0; n < WN; ++n)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[m][n][r] = 0.f;
+
+  int pix_base[WM];
+#pragma unroll
+  for (int m = 0; m < WM; ++m) pix_base[m] = ((wave * WM + m) * a.ic + li) * CS;
+  const float* wcls = a.w + a.wcls[cls];
+  const int nstage = (tile_elems + NT - 1) / NT;
+  __syncthreads();
+
+  for (int ch = 0; ch < a.nchunks; ++ch) {
+    const float* cur = tiles[ch & 1];
+    float* nxt = tiles[(ch + 1) & 1];
+    const bool has_next = ch + 1 < a.nchunks;
+    const float* wch = wcls + (size_t)ch * kbc * a.ntp * 128;
+    float4 A[WM], Bv[WN], An[WM], Bn[WN];
+    auto load = [&](int q, float4 (&Ar)[WM], float4 (&Br)[WN]) {
+      const int kb = 2 * q + lh;
+      const int t = kb / CC4;
+      const int c4 = kb - t * CC4;
+      const int toff = (t < ntaps ? tap_off[t] : 0) + c4 * 4;
+#pragma unroll
+      for (int m = 0; m < WM; ++m) Ar[m] = *reinterpret_cast<const float4*>(cur + pix_base[m] + toff);
+      const float* wk = wch + ((size_t)kb * a.ntp + nt0) * 128 + li * 4;
+#pragma unroll
+      for (int n = 0; n < WN; ++n) Br[n] = *reinterpret_cast<const float4*>(wk + n * 128);
+    };
+    load(0, A, Bv);
+    for (int q = 0; q < nq; ++q) {
+      float4 sv;
+      int sd = -1;
+      if (has_next && q < nstage) {
+        const int e = tid + q * NT;
+        if (e < tile_elems) fetch(e, ch + 1, sv, sd);
+      }
+      if (q + 1 < nq) load(q + 1, An, Bn);
+#pragma unroll
+      for (int m = 0; m < WM; ++m)
+#pragma unroll
+        for (int n = 0; n < WN; ++n) acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x2f32(A[m].x, Bv[n].x, acc[m][n], 0, 0, 0);
+#pragma unroll
+      for (int m = 0; m < WM; ++m)
+#pragma unroll
+        for (int n = 0; n < WN; ++n) acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x2f32(A[m].y, Bv[n].y, acc[m][n], 0, 0, 0);
+#pragma unroll
+      for (int m = 0; m < WM; ++m)
+#pragma unroll
+        for (int n = 0; n < WN; ++n) acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x2f32(A[m].z, Bv[n].z, acc[m][n], 0, 0, 0);
+#pragma unroll
+      for (int m = 0; m < WM; ++m)
+#pragma unroll
+        for (int n = 0; n < WN; ++n) acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x2f32(A[m].w, Bv[n].w, acc[m][n], 0, 0, 0);
+      if (sd >= 0) *reinterpret_cast<float4*>(nxt + sd) = sv;
+#pragma unroll
+      for (int m = 0; m < WM; ++m) A[m] = An[m];
+#pragma unroll
+      for (int n = 0; n < WN; ++n) Bv[n] = Bn[n];
+    }
+    if (has_next) {
+      for (int q = nq; q < nstage; ++q) {
+        const int e = tid + q * NT;
+        if (e < tile_elems) {
+          float4 v;
+          int d;
+          fetch(e, ch + 1, v, d);
+          *reinterpret_cast<float4*>(nxt + d) = v;
+        }
+      }
+    }
+    __syncthreads();
+  }
+
+  const int oy0 = a.oy0[cls], ox0 = a.ox0[cls];
+#pragma unroll
+  for (int n = 0; n < WN; ++n) {
+    const int j = (nt0 + n) * 32 + li;
+    if (j >= a.coutp) continue;
+    const bool real = j < a.cout;
+    const float bj = real ? a.bias[j] : 0.f;
+#pragma unroll
+    for (int m = 0; m < WM; ++m) {
+      const int qy = qy0 + wave * WM + m;
+      if (qy >= a.Hq) continue;
+      const int oy = qy * a.sout + oy0;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int qx = qx0 + (r & 3) + 8 * (r >> 2) + 4 * lh;
         if (qx >= a.Wq) continue;
         const int ox = qx * a.sout + ox0;
         const size_t o = (((size_t)b * a.Ho + oy) * a.Wo + ox) * a.coutp + j;
@@ -321,25 +498,29 @@ __global__ __launch_bounds__(kThreads) void deconv2_mfma_f32_kernel(const ConvAr
   }
 }
 
-// Small-N variant (cout <= 16: SpyNet conv4/conv5, Warp_net conv6, mvDecoder deconv8,
-// resDecoder deconv4). Padding N to an MFMA tile of 32 would waste 2-16x of the matrix work, so
-// this path is VALU: one output pixel per lane, COUTP accumulators in registers, input from the
-// same LDS halo tile as the MFMA kernel (conflict-free ds_read_b128), weights wave-uniform
-// (scalar loads). v_fma_f32 runs at the same per-SIMD rate as the f32 MFMA on gfx950.
+// Small-N variant (cout <= 4: SpyNet conv5, Warp_net conv6, mvDecoder deconv8, resDecoder
+// deconv4). Padding N to an MFMA tile of 32 would waste 8-16x of the matrix work, so this path is
+// VALU: each lane owns a column of PY output pixels x COUTP channels; the chunk's weights are
+// staged in LDS once and read as wave-uniform broadcasts, reused across the PY pixels; the input
+// comes from the same conflict-free LDS halo tile layout as the MFMA kernel.
+constexpr int kSmallPY = 4;
+
 template <int CC, int COUTP>
 __global__ __launch_bounds__(kThreads) void conv_smalln_f32_kernel(const ConvArgs a) {
   using G = ChunkGeom<CC>;
   constexpr int CC4 = G::CC4;
   constexpr int CS = G::CS;
   constexpr int TW = 32;
+  constexpr int PY = kSmallPY;
+  constexpr int TH = (kThreads / TW) * PY;
 
   extern __shared__ __attribute__((aligned(16))) float smem[];
   int* tap_off = reinterpret_cast<int*>(smem);
-  float* tile = smem + 64;
+  float* wl = smem + 64;                                   // [ntaps][CC][COUTP]
+  const int ntaps = a.ntaps[blockIdx.z % a.nclass];
+  float* tile = wl + ((ntaps * CC * COUTP + 3) & ~3);
 
   const int tid = threadIdx.x;
-  const int nthr = blockDim.x;
-  const int TH = nthr / TW;
   const int tx = tid & (TW - 1);
   const int ty = tid / TW;
   const int cls = blockIdx.z % a.nclass;
@@ -347,24 +528,27 @@ __global__ __launch_bounds__(kThreads) void conv_smalln_f32_kernel(const ConvArg
   const int tiles_x = (a.Wq + TW - 1) / TW;
   const int qy0 = (blockIdx.x / tiles_x) * TH;
   const int qx0 = (blockIdx.x % tiles_x) * TW;
-  const int ntaps = a.ntaps[cls];
 
   if (tid < ntaps)
     tap_off[tid] = ((a.tdy[cls][tid] - a.dymin) * a.ic + (a.tdx[cls][tid] - a.dxmin)) * CS;
 
-  float acc[COUTP];
+  float acc[PY][COUTP];
 #pragma unroll
-  for (int j = 0; j < COUTP; ++j) acc[j] = 0.f;
+  for (int k = 0; k < PY; ++k)
+#pragma unroll
+    for (int j = 0; j < COUTP; ++j) acc[k][j] = 0.f;
 
   const int iy0 = qy0 * a.sin + a.dymin;
   const int ix0 = qx0 * a.sin + a.dxmin;
   const int tile_elems = a.ir * a.ic * CC4;
   const float* xb = a.x + (size_t)b * a.H * a.W * a.cinp;
-  const int pix_base = ((ty * a.sin) * a.ic + tx * a.sin) * CS;
+  const int pix_base = ((ty * PY * a.sin) * a.ic + tx * a.sin) * CS;
+  const int row_step = a.sin * a.ic * CS;
   const float* __restrict__ wcls = a.w + a.wcls[cls];
+  const int wl_elems = ntaps * CC * COUTP;
 
   for (int ch = 0; ch < a.nchunks; ++ch) {
-    for (int e = tid; e < tile_elems; e += nthr) {
+    for (int e = tid; e < tile_elems; e += kThreads) {
       const int c4 = e % CC4;
       const int p = e / CC4;
       const int r = p / a.ic;
@@ -378,49 +562,68 @@ __global__ __launch_bounds__(kThreads) void conv_smalln_f32_kernel(const ConvArg
       }
       *reinterpret_cast<float4*>(tile + p * CS + c4 * 4) = v;
     }
+    const float* wch = wcls + (size_t)ch * wl_elems;
+    for (int e = tid; e < wl_elems; e += kThreads) wl[e] = wch[e];
     __syncthreads();
-    const float* __restrict__ wch = wcls + (size_t)ch * ntaps * CC * COUTP;
     for (int t = 0; t < ntaps; ++t) {
-      const int toff = __builtin_amdgcn_readfirstlane(tap_off[t]);
-      const float* __restrict__ wt = wch + t * CC * COUTP;
+      const int toff = tap_off[t];
+      const float* wt = wl + t * CC * COUTP;
 #pragma unroll
       for (int c4 = 0; c4 < CC4; ++c4) {
-        const float4 v = *reinterpret_cast<const float4*>(tile + pix_base + toff + c4 * 4);
-        const float vv[4] = {v.x, v.y, v.z, v.w};
+        float4 v[PY];
 #pragma unroll
-        for (int e = 0; e < 4; ++e)
+        for (int k = 0; k < PY; ++k)
+          v[k] = *reinterpret_cast<const float4*>(tile + pix_base + k * row_step + toff + c4 * 4);
 #pragma unroll
-          for (int j = 0; j < COUTP; ++j) acc[j] = __builtin_fmaf(vv[e], wt[(c4 * 4 + e) * COUTP + j], acc[j]);
+        for (int e = 0; e < 4; ++e) {
+          float wv[COUTP];
+#pragma unroll
+          for (int j4 = 0; j4 < COUTP / 4; ++j4) {
+            const float4 w4 = *reinterpret_cast<const float4*>(wt + (c4 * 4 + e) * COUTP + j4 * 4);
+            wv[j4 * 4] = w4.x; wv[j4 * 4 + 1] = w4.y; wv[j4 * 4 + 2] = w4.z; wv[j4 * 4 + 3] = w4.w;
+          }
+#pragma unroll
+          for (int k = 0; k < PY; ++k) {
+            const float xv = e == 0 ? v[k].x : (e == 1 ? v[k].y : (e == 2 ? v[k].z : v[k].w));
+#pragma unroll
+            for (int j = 0; j < COUTP; ++j) acc[k][j] = __builtin_fmaf(xv, wv[j], acc[k][j]);
+          }
+        }
       }
     }
     __syncthreads();
   }
 
-  const int qy = qy0 + ty, qx = qx0 + tx;
-  if (qy >= a.Hq || qx >= a.Wq) return;
-  const int oy = qy * a.sout + a.oy0[cls];
+  const int qx = qx0 + tx;
+  if (qx >= a.Wq) return;
   const int ox = qx * a.sout + a.ox0[cls];
-  const size_t o = (((size_t)b * a.Ho + oy) * a.Wo + ox) * a.coutp;
 #pragma unroll
-  for (int j4 = 0; j4 < COUTP / 4; ++j4) {
-    float r4[4];
+  for (int k = 0; k < PY; ++k) {
+    const int qy = qy0 + ty * PY + k;
+    if (qy >= a.Hq) continue;
+    const int oy = qy * a.sout + a.oy0[cls];
+    const size_t o = (((size_t)b * a.Ho + oy) * a.Wo + ox) * a.coutp;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int j = j4 * 4 + u;
-      float v = acc[j] + (j < a.cout ? a.bias[j] : 0.f);
-      if (a.act == FVC_ACT_RELU) v = v > 0.f ? v : 0.f;
-      else if (a.act == FVC_ACT_LRELU) v = v > 0.f ? v : 0.1f * v;
-      if (a.res) v += a.res[o + j];
-      if (a.post_op == FVC_POST_EXP) v = expf(v);
-      r4[u] = j < a.cout ? v : 0.f;
+    for (int j4 = 0; j4 < COUTP / 4; ++j4) {
+      float r4[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int j = j4 * 4 + u;
+        float v = acc[k][j] + (j < a.cout ? a.bias[j] : 0.f);
+        if (a.act == FVC_ACT_RELU) v = v > 0.f ? v : 0.f;
+        else if (a.act == FVC_ACT_LRELU) v = v > 0.f ? v : 0.1f * v;
+        if (a.res) v += a.res[o + j];
+        if (a.post_op == FVC_POST_EXP) v = expf(v);
+        r4[u] = j < a.cout ? v : 0.f;
+      }
+      *reinterpret_cast<float4*>(a.y + o + j4 * 4) = make_float4(r4[0], r4[1], r4[2], r4[3]);
     }
-    *reinterpret_cast<float4*>(a.y + o + j4 * 4) = make_float4(r4[0], r4[1], r4[2], r4[3]);
   }
 }
 
 // ------------------------------------------------------------------ host-side geometry
 struct Cfg {
-  int cinp, coutp, ntp, cc, wm, wn, nclass, nchunks, smalln, fused;
+  int cinp, coutp, ntp, cc, wm, wn, nclass, nchunks, smalln, fused, th, pipe, nw, lds_bufs;
   int sin, sout;
   int ntaps[4], kbc[4], oy0[4], ox0[4];
   int tky[4][kMaxTaps], tkx[4][kMaxTaps];  // kernel tap (ky,kx)
@@ -483,20 +686,42 @@ static bool make_cfg(int cin, int cout, int ks, int stride, int transposed, Cfg&
       c.dxmax = c.tdx[cl][t] > c.dxmax ? c.tdx[cl][t] : c.dxmax;
     }
   c.wn = c.ntp;
-  c.smalln = c.coutp <= 16 ? 1 : 0;
+  c.smalln = c.coutp <= 4 ? 1 : 0;  // cout 2/3: MFMA N-tile padding would waste 8-16x
   c.fused = (transposed && stride == 2 && !c.smalln && c.cinp % 8 == 0 && ks <= 5) ? 1 : 0;
   c.wm = ((!transposed && stride == 2) || c.fused) ? 1 : 2;
   if (c.fused) c.wn = (c.ntp % 2 == 0) ? 2 : 1;
-  // channel chunk: largest of {32,16,8,4} dividing cinp whose halo tile fits 64 KB
+  // channel chunk: largest of {32,16,8,4} dividing cinp whose LDS footprint fits 64 KB
+  int maxt = 0;
+  for (int cl = 0; cl < c.nclass; ++cl) maxt = c.ntaps[cl] > maxt ? c.ntaps[cl] : maxt;
+  // pipelined (double-buffered) path for stride-1 convs with >= 2 channel chunks
+  // measured (scripts/conv_micro.py, MI355X): 3x3 128->128 gains +31 % from the 8-wave
+  // pipelined kernel; 3x3 64->64 and the 7x7 layers are faster on the 4-wave single-buffer one.
+  c.pipe = (!transposed && stride == 1 && !c.smalln && c.cinp >= 128 && ks <= 3) ? 1 : 0;
+  c.nw = 8;
+  {
+    const char* v = getenv("FVC_CONV_PIPE");
+    if (v && v[0] == '0') c.pipe = 0;
+    const char* v7 = getenv("FVC_CONV_PIPE7");
+    if (v7 && v7[0] == '1' && !transposed && stride == 1 && !c.smalln && c.cinp >= 32) c.pipe = 1;
+    const char* w = getenv("FVC_CONV_NW");
+    if (c.pipe && w && w[0] == '4') c.nw = 4;
+    const char* p1 = getenv("FVC_CONV_PIPE");
+    if (p1 && p1[0] == '1' && !transposed && stride == 1 && !c.smalln && c.cinp >= 32 && ks <= 3) c.pipe = 1;
+    const char* wn2 = getenv("FVC_CONV_WN2");
+    if (wn2 && wn2[0] == '1' && !c.pipe && !c.smalln && c.ntp == 4) c.wn = 2;
+  }
+  c.lds_bufs = c.pipe ? 2 : 1;
+  c.th = c.smalln ? (kThreads / 32) * kSmallPY : (c.pipe ? c.nw * c.wm : 4 * c.wm);
   int cc = 32;
   for (;; cc >>= 1) {
     if (cc == 4) break;
     if (c.cinp % cc) continue;
-    const int TH = 4 * c.wm;
-    const int ir = (TH - 1) * c.sin + 1 + (c.dymax - c.dymin);
+    const int ir = (c.th - 1) * c.sin + 1 + (c.dymax - c.dymin);
     const int ic = 31 * c.sin + 1 + (c.dxmax - c.dxmin);
     const int cs = ((cc / 4) % 2 == 1) ? cc : cc + 4;
-    if ((size_t)ir * ic * cs * 4 + 256 <= 64 * 1024) break;
+    const size_t wbytes = c.smalln ? (size_t)((maxt * cc * c.coutp + 3) & ~3) * 4 : 0;
+    const size_t budget = c.pipe ? 100 * 1024 : 64 * 1024;
+    if ((size_t)c.lds_bufs * (((size_t)ir * ic * cs + 3) & ~(size_t)3) * 4 + 256 + wbytes <= budget) break;
   }
   c.cc = cc;
   c.nchunks = c.cinp / cc;
@@ -555,6 +780,43 @@ static int launch_sn_n(int coutp, const ConvArgs& a, dim3 grid, dim3 blk, size_t
   return FVC_EINVAL;
 }
 
+template <int CC, int WN, int NW>
+static int launch_pp_t(const ConvArgs& a, dim3 grid, size_t lds, hipStream_t s) {
+  if (lds > 64 * 1024) hipFuncSetAttribute((const void*)conv_mfma_pipe_kernel<CC, 2, WN, NW>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL((conv_mfma_pipe_kernel<CC, 2, WN, NW>), grid, dim3(NW * 64), lds, s, a);
+  FVC_CHECK_LAUNCH();
+  return 0;
+}
+
+template <int CC, int NW>
+static int launch_pp_wn(int wn, const ConvArgs& a, dim3 grid, size_t lds, hipStream_t s) {
+  switch (wn) {
+    case 1: return launch_pp_t<CC, 1, NW>(a, grid, lds, s);
+    case 2: return launch_pp_t<CC, 2, NW>(a, grid, lds, s);
+    case 3: return launch_pp_t<CC, 3, NW>(a, grid, lds, s);
+    case 4: return launch_pp_t<CC, 4, NW>(a, grid, lds, s);
+  }
+  return FVC_EINVAL;
+}
+
+static int launch_pipe(int cc, int wn, int nw, const ConvArgs& a, dim3 grid, size_t lds, hipStream_t s) {
+  if (nw == 8) {
+    switch (cc) {
+      case 8: return launch_pp_wn<8, 8>(wn, a, grid, lds, s);
+      case 16: return launch_pp_wn<16, 8>(wn, a, grid, lds, s);
+      case 32: return launch_pp_wn<32, 8>(wn, a, grid, lds, s);
+    }
+  } else {
+    switch (cc) {
+      case 8: return launch_pp_wn<8, 4>(wn, a, grid, lds, s);
+      case 16: return launch_pp_wn<16, 4>(wn, a, grid, lds, s);
+      case 32: return launch_pp_wn<32, 4>(wn, a, grid, lds, s);
+    }
+  }
+  return FVC_EINVAL;
+}
+
 template <int CC, int WN>
 static int launch_fd_t(const ConvArgs& a, dim3 grid, size_t lds, hipStream_t s) {
   hipLaunchKernelGGL((deconv2_mfma_f32_kernel<CC, WN>), grid, dim3(kThreads), lds, s, a);
@@ -609,7 +871,7 @@ static int run_conv(const float* x, const float* wpack, const float* bias, const
   }
   a.sin = c.sin; a.sout = c.sout; a.nclass = c.nclass; a.nchunks = c.nchunks; a.ntp = c.ntp;
   a.dymin = c.dymin; a.dxmin = c.dxmin;
-  const int TH = 4 * c.wm;
+  const int TH = c.th;
   a.ir = (TH - 1) * c.sin + 1 + (c.dymax - c.dymin);
   a.ic = 31 * c.sin + 1 + (c.dxmax - c.dxmin);
   a.in_op = in_op; a.act = act; a.post_op = post_op;
@@ -626,16 +888,23 @@ static int run_conv(const float* x, const float* wpack, const float* bias, const
     }
   }
   const int cs = ((c.cc / 4) % 2 == 1) ? c.cc : c.cc + 4;
-  const size_t lds = 256 + (size_t)a.ir * a.ic * cs * 4;
+  int maxt = 0;
+  for (int cl = 0; cl < c.nclass; ++cl) maxt = c.ntaps[cl] > maxt ? c.ntaps[cl] : maxt;
+  const size_t wbytes = c.smalln ? (size_t)((maxt * c.cc * c.coutp + 3) & ~3) * 4 : 0;
+  const size_t lds = 256 + wbytes + (size_t)c.lds_bufs * (((size_t)a.ir * a.ic * cs + 3) & ~(size_t)3) * 4;
   const int tiles_x = fvc_cdiv(a.Wq, 32);
   const int tiles_y = fvc_cdiv(a.Hq, TH);
   if (c.smalln) {
     dim3 grid(tiles_x * tiles_y, 1, batch * c.nclass);
-    return launch_smalln(c.cc, c.coutp, a, grid, dim3(TH * 32), lds, s);
+    return launch_smalln(c.cc, c.coutp, a, grid, dim3(kThreads), lds, s);
   }
   if (c.fused) {
     dim3 grid(tiles_x * tiles_y, c.ntp / c.wn, batch);
     return launch_fused(c.cc, c.wn, a, grid, lds, s);
+  }
+  if (c.pipe) {
+    dim3 grid(tiles_x * tiles_y, c.ntp / c.wn, batch * c.nclass);
+    return launch_pipe(c.cc, c.wn, c.nw, a, grid, lds, s);
   }
   dim3 grid(tiles_x * tiles_y, c.ntp / c.wn, batch * c.nclass);
   switch (c.cc) {

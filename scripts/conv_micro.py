@@ -1,0 +1,44 @@
+"""Micro-benchmark of single conv geometries at 1080p (for rocprofv3 --pmc / timing)."""
+import argparse
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from fastvideocodec_amd import kernels as K  # noqa: E402
+from fastvideocodec_amd.profiling import conv_flops  # noqa: E402
+
+CASES = {
+    "c3_64_full": (64, 64, 3, 1, False, 1088, 1920),
+    "c3_128_half": (128, 128, 3, 1, False, 544, 960),
+    "c7_32_64_full": (32, 64, 7, 1, False, 1088, 1920),
+    "d3_128_half": (128, 128, 3, 2, True, 544, 960),
+    "c3_128_2_full": (128, 2, 3, 1, False, 1088, 1920),
+    "c7_32_16_full": (32, 16, 7, 1, False, 1088, 1920),
+}
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--cases", default=",".join(CASES))
+ap.add_argument("--iters", type=int, default=10)
+args = ap.parse_args()
+dev = torch.device("cuda")
+for name in args.cases.split(","):
+    cin, cout, k, s, tr, H, W = CASES[name]
+    if tr:
+        H, W = H // 2, W // 2
+    w = torch.randn((cin, cout, k, k) if tr else (cout, cin, k, k)) * 0.05
+    pc = K.PackedConv(w, torch.zeros(cout), k, s, tr, dev)
+    x = torch.randn(1, H, W, K.cp4(cin), device=dev)
+    y = pc(x)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(args.iters):
+        pc(x, out=y)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / args.iters
+    fl = conv_flops(cin, cout, k, s, tr, 1, H, W)
+    print(f"{name:16s} {ms:8.3f} ms  {fl / ms / 1e9:8.2f} TF/s", flush=True)
