@@ -720,8 +720,15 @@ static bool make_cfg(int cin, int cout, int ks, int stride, int transposed, Cfg&
     const int ic = 31 * c.sin + 1 + (c.dxmax - c.dxmin);
     const int cs = ((cc / 4) % 2 == 1) ? cc : cc + 4;
     const size_t wbytes = c.smalln ? (size_t)((maxt * cc * c.coutp + 3) & ~3) * 4 : 0;
-    const size_t budget = c.pipe ? 100 * 1024 : 64 * 1024;
+    const size_t budget = (c.pipe && c.nw == 8) ? 100 * 1024 : 64 * 1024;
     if ((size_t)c.lds_bufs * (((size_t)ir * ic * cs + 3) & ~(size_t)3) * 4 + 256 + wbytes <= budget) break;
+  }
+  {
+    const char* vcc = getenv("FVC_CONV_CC");  // experiment override (must stay fixed per process)
+    if (vcc && !c.smalln && !c.fused) {
+      const int want = atoi(vcc);
+      if ((want == 8 || want == 16 || want == 32) && c.cinp % want == 0) cc = want;
+    }
   }
   c.cc = cc;
   c.nchunks = c.cinp / cc;

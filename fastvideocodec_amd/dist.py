@@ -1,0 +1,60 @@
+"""Multi-GPU plumbing for GOP-sharded coding.
+
+GOPs are independent (each starts from its own I-frame; the only dependency, ``x_prev``, is inside
+a GOP, ``models.py:372-376``), so ranks never exchange data while coding. After coding, one
+collective round moves the small results: the per-rank elapsed time (MAX), per-rank metrics
+(all_gather) and, optionally, every rank's bitstream bytes to rank 0 (all_gather of lengths, then
+all_gather of zero-padded payloads — a few hundred KB per frame, latency-bound on xGMI).
+Works with ``nccl`` (RCCL on ROCm; device tensors) and ``gloo`` (CPU tensors, tests).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+
+def shard_gops(n_gops: int, rank: int, world: int):
+    """GOP g goes to rank g % world (round-robin)."""
+    return [g for g in range(n_gops) if g % world == rank]
+
+
+def _dev(device):
+    return torch.device(device) if device is not None else torch.device("cpu")
+
+
+def max_over_ranks(value: float, device=None) -> float:
+    t = torch.tensor([value], dtype=torch.float64, device=_dev(device))
+    if dist.is_initialized() and dist.get_world_size() > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def gather_stats(stats, device=None):
+    """all_gather a 1-D float64 vector of per-rank statistics -> [world, n] numpy array."""
+    t = torch.as_tensor(np.asarray(stats, np.float64), device=_dev(device))
+    if not (dist.is_initialized() and dist.get_world_size() > 1):
+        return t.cpu().numpy()[None]
+    out = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, t)
+    return torch.stack(out).cpu().numpy()
+
+
+def gather_bytes(payload: bytes, device=None):
+    """Every rank contributes one byte string; returns the list of all ranks' strings (on every
+    rank). Two collectives: lengths, then zero-padded payloads."""
+    dev = _dev(device)
+    if not (dist.is_initialized() and dist.get_world_size() > 1):
+        return [payload]
+    world = dist.get_world_size()
+    n = torch.tensor([len(payload)], dtype=torch.int64, device=dev)
+    lens = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(lens, n)
+    lens = [int(x.item()) for x in lens]
+    cap = max(max(lens), 1)
+    buf = torch.zeros(cap, dtype=torch.uint8, device=dev)
+    if payload:
+        buf[: len(payload)] = torch.frombuffer(bytearray(payload), dtype=torch.uint8).to(dev)
+    outs = [torch.zeros_like(buf) for _ in range(world)]
+    dist.all_gather(outs, buf)
+    return [bytes(o[:L].cpu().numpy().tobytes()) for o, L in zip(outs, lens)]
