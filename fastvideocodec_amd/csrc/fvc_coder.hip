@@ -73,12 +73,38 @@ __device__ __forceinline__ bool enc_put_bits(uint64_t& x, uint32_t*& ptr, const 
   return true;
 }
 
-// Phase 1 (fully parallel over all symbols): table lookups. prep[i] = start | freq << 16,
-// raw[i] = escape payload. The escape bin is the only one ending at 1<<16, so the sequential
-// phase recognises it from start + freq == 65536 without another array.
+// Phase 1 (fully parallel over all symbols): table lookups plus ryg_rans' reciprocal form of
+// the division (Rans64EncSymbolInit: q = mulhi64(x, rcp) >> shift, exact for every x the coder
+// can hold), so the sequential phase has no divide on its critical path.
+struct EncSym {
+  uint64_t rcp;     // rcp_freq
+  uint32_t sf;      // start | freq << 16
+  uint32_t shift;   // rcp_shift | escape flag << 8
+};
+
+__device__ __forceinline__ EncSym make_enc_sym(uint32_t start, uint32_t freq, bool esc) {
+  EncSym e;
+  e.sf = start | (freq << 16);
+  if (freq < 2) {
+    e.rcp = ~0ull;
+    e.shift = 0;
+  } else {
+    uint32_t shift = 0;
+    while (freq > (1u << shift)) shift++;
+    uint64_t x0 = freq - 1, x1 = 1ull << (shift + 31);
+    const uint64_t t1 = x1 / freq;
+    x0 += (x1 % freq) << 32;
+    const uint64_t t0 = x0 / freq;
+    e.rcp = t0 + (t1 << 32);
+    e.shift = shift - 1;
+  }
+  if (esc) e.shift |= 0x100u;
+  return e;
+}
+
 __global__ void k_rans_prep(const int32_t* __restrict__ symbols, const int32_t* __restrict__ indexes, int64_t n,
                             const int32_t* __restrict__ cdfs, int cdf_stride, const int32_t* __restrict__ cdf_sizes,
-                            const int32_t* __restrict__ offsets, uint32_t* __restrict__ prep,
+                            const int32_t* __restrict__ offsets, EncSym* __restrict__ prep,
                             uint32_t* __restrict__ raw_out) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const int32_t ci = indexes[i];
@@ -94,31 +120,17 @@ __global__ void k_rans_prep(const int32_t* __restrict__ symbols, const int32_t* 
       value = max_value;
     }
     const uint32_t start = (uint32_t)cdf[value];
-    const uint32_t freq = (uint32_t)(cdf[value + 1] - cdf[value]);
-    prep[i] = start | (freq << 16);  // freq < 65536 (every table has >= 2 bins)
+    const uint32_t freq = (uint32_t)(cdf[value + 1] - cdf[value]);  // < 65536: every table has >= 2 bins
+    prep[i] = make_enc_sym(start, freq, value == max_value);
     raw_out[i] = raw;
   }
 }
 
-// x / freq, x % freq for x < 2^63, 0 < freq < 2^16 without a generic 64-bit divide:
-// high word by a 32-bit divide, low part (< freq * 2^32 < 2^48, exact in f64) by an f64
-// reciprocal estimate + one-step remainder correction.
-__device__ __forceinline__ void udivmod64_16(uint64_t x, uint32_t freq, double rcp, uint64_t& q, uint32_t& r) {
-  const uint32_t hi = (uint32_t)(x >> 32);
-  const uint32_t qh = hi / freq;
-  const uint32_t rh = hi - qh * freq;
-  const uint64_t t = ((uint64_t)rh << 32) | (uint32_t)x;
-  uint32_t ql = (uint32_t)((double)t * rcp);
-  int64_t rr = (int64_t)t - (int64_t)((uint64_t)ql * freq);
-  if (rr < 0) { ql -= 1; rr += freq; }
-  else if (rr >= (int64_t)freq) { ql += 1; rr -= freq; }
-  q = ((uint64_t)qh << 32) + ql;
-  r = (uint32_t)rr;
-}
+__device__ __forceinline__ uint64_t mulhi64(uint64_t a, uint64_t b) { return __umul64hi(a, b); }
 
 // Phase 2: one lane per stream walks its symbols backward (compressai's BufferedRansEncoder
 // pushes forward and flushes backward; each symbol's sub-symbols are put in reverse push order).
-__global__ void k_rans_encode(const uint32_t* __restrict__ prep, const uint32_t* __restrict__ raw_in,
+__global__ void k_rans_encode(const EncSym* __restrict__ prep, const uint32_t* __restrict__ raw_in,
                               const int64_t* __restrict__ sym_off, int nstreams, uint32_t* __restrict__ words,
                               const int64_t* __restrict__ word_off, int32_t* __restrict__ nwords) {
   const int s = blockIdx.x * blockDim.x + threadIdx.x;
@@ -130,12 +142,13 @@ __global__ void k_rans_encode(const uint32_t* __restrict__ prep, const uint32_t*
   bool ok = true;
   const int64_t b = sym_off[s];
   int64_t i = sym_off[s + 1] - 1;
-  uint32_t pnext = i >= b ? prep[i] : 0;
+  EncSym pnext;
+  if (i >= b) pnext = prep[i];
   for (; ok && i >= b; --i) {
-    const uint32_t p = pnext;
+    const EncSym p = pnext;
     if (i > b) pnext = prep[i - 1];  // prefetch: independent of the state chain
-    const uint32_t start = p & 0xFFFFu, freq = p >> 16;
-    if (start + freq == (1u << kPrec)) {  // escape bin: bypass-coded payload
+    const uint32_t start = p.sf & 0xFFFFu, freq = p.sf >> 16;
+    if (p.shift & 0x100u) {  // escape bin: bypass-coded payload
       const uint32_t raw = raw_in[i];
       int32_t nb = 0;
       while (nb < 8 && (raw >> (nb * kBypassPrec)) != 0) ++nb;
@@ -151,10 +164,10 @@ __global__ void k_rans_encode(const uint32_t* __restrict__ prep, const uint32_t*
       *--ptr = (uint32_t)x;
       x >>= 32;
     }
-    uint64_t q;
-    uint32_t r;
-    udivmod64_16(x, freq, 1.0 / (double)freq, q, r);
-    x = (q << kPrec) + r + start;
+    // Rans64EncPutSymbol: x = x + bias + q * (2^prec - freq), q = mulhi(x, rcp) >> shift
+    const uint64_t q = mulhi64(x, p.rcp) >> (p.shift & 0xFFu);
+    const uint64_t bias = freq < 2 ? (uint64_t)start + (1u << kPrec) - 1 : (uint64_t)start;
+    x = x + bias + q * (uint64_t)((1u << kPrec) - freq);
   }
   if (ok && ptr - lo >= 2) {
     ptr -= 2;
@@ -204,9 +217,12 @@ __global__ void k_pack_copy(const uint32_t* __restrict__ words, const int64_t* _
 }
 
 
-// Decode LUT: lut[t][cum] = the symbol s of table t with cdf[s] <= cum < cdf[s+1].
+// Decode LUTs: lut[t][cum] = the symbol s of table t with cdf[s] <= cum < cdf[s+1], and
+// lutsf[t][cum] = cdf[s] | (cdf[s+1]-cdf[s]) << 16. The state update needs only lutsf, so each
+// decoded symbol costs one dependent load (lut, needed only for the output value, is issued in
+// parallel and is off the state chain).
 __global__ void k_build_lut(const int32_t* __restrict__ cdfs, int cdf_stride, const int32_t* __restrict__ cdf_sizes,
-                            int ntables, uint16_t* __restrict__ lut) {
+                            int ntables, uint16_t* __restrict__ lut, uint32_t* __restrict__ lutsf) {
   const int64_t n = (int64_t)ntables << kPrec;
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
     const int t = (int)(e >> kPrec);
@@ -218,6 +234,7 @@ __global__ void k_build_lut(const int32_t* __restrict__ cdfs, int cdf_stride, co
       if ((uint32_t)cdf[mid] <= cum) lo = mid; else hi = mid;
     }
     lut[e] = (uint16_t)lo;
+    lutsf[e] = (uint32_t)cdf[lo] | ((uint32_t)(cdf[lo + 1] - cdf[lo]) << 16);
   }
 }
 
@@ -231,8 +248,8 @@ __device__ __forceinline__ bool dec_renorm(uint64_t& x, const uint32_t*& ptr, co
 
 __global__ void k_rans_decode(const uint32_t* __restrict__ packed, const int64_t* __restrict__ pack_off,
                               const int32_t* __restrict__ indexes, const int64_t* __restrict__ sym_off, int nstreams,
-                              const int32_t* __restrict__ cdfs, int cdf_stride, const int32_t* __restrict__ cdf_sizes,
-                              const int32_t* __restrict__ offsets, const uint16_t* __restrict__ lut,
+                              const int32_t* __restrict__ cdf_sizes, const int32_t* __restrict__ offsets,
+                              const uint16_t* __restrict__ lut, const uint32_t* __restrict__ lutsf,
                               int32_t* __restrict__ symbols, int32_t* __restrict__ status) {
   const int s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= nstreams) return;
@@ -255,15 +272,15 @@ __global__ void k_rans_decode(const uint32_t* __restrict__ packed, const int64_t
       symbols[i] = 0;
       continue;
     }
-    const int32_t* cdf = cdfs + (size_t)ci * cdf_stride;
-    const int32_t max_value = cdf_sizes[ci] - 2;
     const uint32_t cum = (uint32_t)(x & mask);
-    const int32_t sidx = lut[((size_t)ci << kPrec) | cum];
-    const uint32_t start = (uint32_t)cdf[sidx], freq = (uint32_t)(cdf[sidx + 1] - cdf[sidx]);
-    x = freq * (x >> kPrec) + (x & mask) - start;
+    const size_t li = ((size_t)ci << kPrec) | cum;
+    const uint32_t sf = lutsf[li];
+    const int32_t sidx = lut[li];
+    const uint32_t start = sf & 0xFFFFu, freq = sf >> 16;
+    x = freq * (x >> kPrec) + cum - start;
     ok = dec_renorm(x, ptr, end);
     int32_t value = sidx;
-    if (ok && value == max_value) {
+    if (ok && start + freq == (1u << kPrec)) {  // escape bin (== max_value)
       auto getbits = [&](int32_t& v) {
         v = (int32_t)(x & kMaxBypass);
         x >>= kBypassPrec;
@@ -282,6 +299,7 @@ __global__ void k_rans_decode(const uint32_t* __restrict__ packed, const int64_t
         ok = getbits(v);
         raw |= (uint32_t)v << (j * kBypassPrec);
       }
+      const int32_t max_value = cdf_sizes[ci] - 2;
       value = (int32_t)(raw >> 1);
       if (raw & 1) value = -value - 1;
       else value += max_value;
@@ -338,7 +356,7 @@ int fvc_channel_indexes(int32_t* idx, int batch, int hw, int c, fvc_stream_t s) 
   return 0;
 }
 
-size_t fvc_rans_encode_ws_bytes(int64_t nsymbols) { return (size_t)nsymbols * 8; }
+size_t fvc_rans_encode_ws_bytes(int64_t nsymbols) { return (size_t)nsymbols * (sizeof(EncSym) + 4); }
 
 int fvc_rans_encode(const int32_t* symbols, const int32_t* indexes, const int64_t* sym_off, int nstreams,
                     int64_t nsymbols, const int32_t* cdfs, int cdf_stride, const int32_t* cdf_sizes,
@@ -347,8 +365,8 @@ int fvc_rans_encode(const int32_t* symbols, const int32_t* indexes, const int64_
   if (!symbols || !indexes || !sym_off || !cdfs || !cdf_sizes || !offsets || !ws || !words || !word_off ||
       !nwords || nstreams <= 0 || nsymbols < 0)
     return FVC_EINVAL;
-  uint32_t* prep = (uint32_t*)ws;
-  uint32_t* raw = prep + nsymbols;
+  EncSym* prep = (EncSym*)ws;
+  uint32_t* raw = (uint32_t*)(prep + nsymbols);
   if (nsymbols > 0) {
     hipLaunchKernelGGL(k_rans_prep, dim3(grid_for((size_t)nsymbols)), dim3(kBlk), 0, (hipStream_t)s, symbols, indexes,
                        nsymbols, cdfs, cdf_stride, cdf_sizes, offsets, prep, raw);
@@ -361,13 +379,15 @@ int fvc_rans_encode(const int32_t* symbols, const int32_t* indexes, const int64_
   return 0;
 }
 
-size_t fvc_rans_lut_bytes(int ntables) { return (size_t)ntables << 17; }
+size_t fvc_rans_lut_bytes(int ntables) { return (size_t)ntables * (6u << kPrec); }
 
-int fvc_rans_build_lut(const int32_t* cdfs, int cdf_stride, const int32_t* cdf_sizes, int ntables, uint16_t* lut,
+int fvc_rans_build_lut(const int32_t* cdfs, int cdf_stride, const int32_t* cdf_sizes, int ntables, void* lut,
                        fvc_stream_t s) {
   if (!cdfs || !cdf_sizes || !lut || ntables <= 0) return FVC_EINVAL;
+  uint32_t* lutsf = (uint32_t*)lut;
+  uint16_t* lut16 = (uint16_t*)(lutsf + ((size_t)ntables << kPrec));
   hipLaunchKernelGGL(k_build_lut, dim3(grid_for((size_t)ntables << 16)), dim3(kBlk), 0, (hipStream_t)s, cdfs,
-                     cdf_stride, cdf_sizes, ntables, lut);
+                     cdf_stride, cdf_sizes, ntables, lut16, lutsf);
   FVC_CHECK_LAUNCH();
   return 0;
 }
@@ -384,14 +404,16 @@ int fvc_rans_pack(const uint32_t* words, const int64_t* word_off, const int32_t*
 }
 
 int fvc_rans_decode(const uint32_t* packed, const int64_t* pack_off, const int32_t* indexes, const int64_t* sym_off,
-                    int nstreams, const int32_t* cdfs, int cdf_stride, const int32_t* cdf_sizes,
-                    const int32_t* offsets, const uint16_t* lut, int32_t* symbols, int32_t* status, fvc_stream_t s) {
-  if (!packed || !pack_off || !indexes || !sym_off || !cdfs || !cdf_sizes || !offsets || !lut || !symbols ||
-      !status || nstreams <= 0)
+                    int nstreams, int ntables, const int32_t* cdf_sizes, const int32_t* offsets, const void* lut,
+                    int32_t* symbols, int32_t* status, fvc_stream_t s) {
+  if (!packed || !pack_off || !indexes || !sym_off || !cdf_sizes || !offsets || !lut || !symbols || !status ||
+      nstreams <= 0 || ntables <= 0)
     return FVC_EINVAL;
+  const uint32_t* lutsf = (const uint32_t*)lut;
+  const uint16_t* lut16 = (const uint16_t*)(lutsf + ((size_t)ntables << kPrec));
   const int blk = 64;
   hipLaunchKernelGGL(k_rans_decode, dim3((nstreams + blk - 1) / blk), dim3(blk), 0, (hipStream_t)s, packed, pack_off,
-                     indexes, sym_off, nstreams, cdfs, cdf_stride, cdf_sizes, offsets, lut, symbols, status);
+                     indexes, sym_off, nstreams, cdf_sizes, offsets, lut16, lutsf, symbols, status);
   FVC_CHECK_LAUNCH();
   return 0;
 }

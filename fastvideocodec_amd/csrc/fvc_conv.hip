@@ -60,7 +60,7 @@ struct ChunkGeom {
   static constexpr int CS = (CC4 % 2 == 1) ? CC : CC + 4;  // LDS pixel stride (floats)
 };
 
-template <int CC, int WM, int WN>
+template <int CC, int WM, int WN, int BPF>
 __global__ __launch_bounds__(kThreads) void conv_mfma_f32_kernel(const ConvArgs a) {
   using G = ChunkGeom<CC>;
   constexpr int CC4 = G::CC4;
@@ -131,21 +131,31 @@ __global__ __launch_bounds__(kThreads) void conv_mfma_f32_kernel(const ConvArgs 
     __syncthreads();
 
     const float* wch = wcls + (size_t)ch * kbc * a.ntp * 128;
-    float4 A[WM], Bv[WN], An[WM], Bn[WN];
-    auto load = [&](int q, float4 (&Ar)[WM], float4 (&Br)[WN]) {
+    float4 A[WM], Bv[WN], An[WM], Bn[WN], Bnn[WN];
+    auto loadA = [&](int q, float4 (&Ar)[WM]) {
       const int kb = 2 * q + lh;
       const int t = kb / CC4;
       const int c4 = kb - t * CC4;
       const int toff = (t < ntaps ? tap_off[t] : 0) + c4 * 4;
 #pragma unroll
       for (int m = 0; m < WM; ++m) Ar[m] = *reinterpret_cast<const float4*>(tile + pix_base[m] + toff);
+    };
+    auto loadB = [&](int q, float4 (&Br)[WN]) {
+      const int kb = 2 * q + lh;
       const float* wk = wch + ((size_t)kb * a.ntp + nt0) * 128 + li * 4;
 #pragma unroll
       for (int n = 0; n < WN; ++n) Br[n] = *reinterpret_cast<const float4*>(wk + n * 128);
     };
-    load(0, A, Bv);
+    loadA(0, A);
+    loadB(0, Bv);
+    if (BPF == 2 && nq > 1) loadB(1, Bn);
     for (int q = 0; q < nq; ++q) {
-      if (q + 1 < nq) load(q + 1, An, Bn);
+      if (q + 1 < nq) loadA(q + 1, An);
+      if (BPF == 2) {
+        if (q + 2 < nq) loadB(q + 2, Bnn);
+      } else {
+        if (q + 1 < nq) loadB(q + 1, Bn);
+      }
       // element-major issue order: consecutive MFMAs hit different accumulators (no RAW chain)
 #pragma unroll
       for (int m = 0; m < WM; ++m)
@@ -166,7 +176,10 @@ __global__ __launch_bounds__(kThreads) void conv_mfma_f32_kernel(const ConvArgs 
 #pragma unroll
       for (int m = 0; m < WM; ++m) A[m] = An[m];
 #pragma unroll
-      for (int n = 0; n < WN; ++n) Bv[n] = Bn[n];
+      for (int n = 0; n < WN; ++n) {
+        Bv[n] = Bn[n];
+        if (BPF == 2) Bn[n] = Bnn[n];
+      }
     }
     __syncthreads();
   }
@@ -688,7 +701,17 @@ static bool make_cfg(int cin, int cout, int ks, int stride, int transposed, Cfg&
   c.wn = c.ntp;
   c.smalln = c.coutp <= 4 ? 1 : 0;  // cout 2/3: MFMA N-tile padding would waste 8-16x
   c.fused = (transposed && stride == 2 && !c.smalln && c.cinp % 8 == 0 && ks <= 5) ? 1 : 0;
+  {
+    // measured: the per-class launch with WN<=2 beats the 4-class fused block (register-bound
+    // at 1 wave/SIMD); keep the fused kernel behind FVC_DECONV_FUSED=1 for experiments.
+    const char* f = getenv("FVC_DECONV_FUSED");
+    c.fused = (f && f[0] == '1') ? c.fused : 0;
+  }
   c.wm = ((!transposed && stride == 2) || c.fused) ? 1 : 2;
+  {
+    const char* w4 = getenv("FVC_CONV_WM4");
+    if (w4 && w4[0] == '1' && !transposed && stride == 1 && ks == 3 && c.ntp <= 2) c.wm = 4;
+  }
   if (c.fused) c.wn = (c.ntp % 2 == 0) ? 2 : 1;
   // channel chunk: largest of {32,16,8,4} dividing cinp whose LDS footprint fits 64 KB
   int maxt = 0;
@@ -708,7 +731,9 @@ static bool make_cfg(int cin, int cout, int ks, int stride, int transposed, Cfg&
     const char* p1 = getenv("FVC_CONV_PIPE");
     if (p1 && p1[0] == '1' && !transposed && stride == 1 && !c.smalln && c.cinp >= 32 && ks <= 3) c.pipe = 1;
     const char* wn2 = getenv("FVC_CONV_WN2");
-    if (wn2 && wn2[0] == '1' && !c.pipe && !c.smalln && c.ntp == 4) c.wn = 2;
+    if (wn2 && wn2[0] == '1' && !c.pipe && !c.smalln && !c.fused && c.ntp == 4) c.wn = 2;
+    const char* wn1 = getenv("FVC_CONV_WN1");
+    if (wn1 && wn1[0] == '1' && !c.smalln) c.wn = 1;
   }
   c.lds_bufs = c.pipe ? 2 : 1;
   c.th = c.smalln ? (kThreads / 32) * kSmallPY : (c.pipe ? c.nw * c.wm : 4 * c.wm);
@@ -745,9 +770,18 @@ static bool make_cfg(int cin, int cout, int ks, int stride, int transposed, Cfg&
   return true;
 }
 
+static int g_bpf = -1;
+
 template <int CC, int WM, int WN>
 static int launch_t(const ConvArgs& a, dim3 grid, size_t lds, hipStream_t s) {
-  hipLaunchKernelGGL((conv_mfma_f32_kernel<CC, WM, WN>), grid, dim3(kThreads), lds, s, a);
+  if (g_bpf < 0) {
+    const char* v = getenv("FVC_CONV_BPF");
+    g_bpf = (v && v[0] == '2') ? 2 : 1;  // measured: 2-deep weight prefetch is 2-4 % slower
+  }
+  if (g_bpf == 2)
+    hipLaunchKernelGGL((conv_mfma_f32_kernel<CC, WM, WN, 2>), grid, dim3(kThreads), lds, s, a);
+  else
+    hipLaunchKernelGGL((conv_mfma_f32_kernel<CC, WM, WN, 1>), grid, dim3(kThreads), lds, s, a);
   FVC_CHECK_LAUNCH();
   return 0;
 }
@@ -766,6 +800,11 @@ static int launch_wn(int wn, const ConvArgs& a, dim3 grid, size_t lds, hipStream
 template <int CC>
 static int launch_wm(int wm, int wn, const ConvArgs& a, dim3 grid, size_t lds, hipStream_t s) {
   if (wm == 1) return launch_wn<CC, 1>(wn, a, grid, lds, s);
+  if (wm == 4) {
+    if (wn == 1) return launch_t<CC, 4, 1>(a, grid, lds, s);
+    if (wn == 2) return launch_t<CC, 4, 2>(a, grid, lds, s);
+    return FVC_EINVAL;
+  }
   return launch_wn<CC, 2>(wn, a, grid, lds, s);
 }
 
@@ -901,6 +940,20 @@ static int run_conv(const float* x, const float* wpack, const float* bias, const
   const size_t lds = 256 + wbytes + (size_t)c.lds_bufs * (((size_t)a.ir * a.ic * cs + 3) & ~(size_t)3) * 4;
   const int tiles_x = fvc_cdiv(a.Wq, 32);
   const int tiles_y = fvc_cdiv(a.Hq, TH);
+  // N-split heuristic (measured, scripts/conv_micro.py): fewer N-tiles per block when the grid
+  // would not fill the chip, and at most 2 for the per-class transposed launch.
+  if (!c.smalln && !c.fused && !getenv("FVC_CONV_WN1") && !getenv("FVC_CONV_WN2")) {
+    int wn = c.ntp;
+    if (transposed && wn == 4) wn = 2;
+    const long long base = (long long)tiles_x * tiles_y * batch * c.nclass;
+    const long long want = c.pipe ? 512 : 1024;
+    while (wn > 1 && base * (c.ntp / wn) < want) {
+      int w2 = wn - 1;
+      while (w2 > 1 && c.ntp % w2) --w2;
+      wn = w2;
+    }
+    c.wn = wn;
+  }
   if (c.smalln) {
     dim3 grid(tiles_x * tiles_y, 1, batch * c.nclass);
     return launch_smalln(c.cc, c.coutp, a, grid, dim3(kThreads), lds, s);

@@ -229,3 +229,22 @@ def test_rans_compressai_api(dev):
     s = EM.RansEncoder(dev).encode_with_indexes(sym, idx, cdfs, list(ft.cdf_length), list(ft.offset))
     assert s == R.rans_encode_py(sym, idx, ft.cdf, ft.cdf_length, ft.offset)
     assert EM.RansDecoder(dev).decode_with_indexes(s, idx, cdfs, list(ft.cdf_length), list(ft.offset)) == sym
+
+
+def test_rans_decode_tails_and_escapes(dev):
+    """Factorized per-channel streams with heavy tails + escapes, and wide Laplace symbols."""
+    rng = np.random.default_rng(13)
+    ft = EM.FactorizedTables(rng.normal(0, 0.01, (11, 8)).astype(np.float32))
+    coder = EM.RangeCoder(ft.cdf, ft.cdf_length, ft.offset, dev)
+    S, n = 40, 700
+    sym = np.round(rng.normal(0, 25, (S, n))).astype(np.int32)
+    sym.flat[rng.integers(0, S * n, 60)] = rng.integers(-5000, 5000, 60)
+    idx = np.repeat((np.arange(S) % 8)[:, None], n, 1).astype(np.int32)
+    enc = coder.encode(torch.from_numpy(sym).to(dev), torch.from_numpy(idx).to(dev))
+    assert (coder.decode(enc, torch.from_numpy(idx).to(dev)).cpu().numpy() == sym).all()
+    lt = EM.LaplaceTables()
+    lc = EM.RangeCoder(lt.cdf, lt.cdf_length, lt.offset, dev)
+    sym = np.round(rng.laplace(0, 60, (S, n))).astype(np.int32)
+    idx = rng.integers(0, 64, (S, n)).astype(np.int32)
+    enc = lc.encode(torch.from_numpy(sym).to(dev), torch.from_numpy(idx).to(dev))
+    assert (lc.decode(enc, torch.from_numpy(idx).to(dev)).cpu().numpy() == sym).all()
