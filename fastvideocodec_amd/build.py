@@ -1,34 +1,60 @@
-"""Build libfvc.so in-tree with hipcc for gfx950 (no JIT cache: the .so travels with the repo)."""
+"""Build libfvc.so in-tree with hipcc for gfx950 (no JIT cache: the .so travels with the repo).
+
+Each source compiles to its own object (in parallel, only when stale), then one link step.
+"""
 from __future__ import annotations
 
 import os
 import subprocess
 import sys
+from concurrent.futures import ThreadPoolExecutor
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-SRCS = ["fvc_conv.hip", "fvc_elem.hip", "fvc_coder.hip"]
+SRCS = ["fvc_conv.hip", "fvc_conv_x3.hip", "fvc_elem.hip", "fvc_coder.hip"]
 OUT = os.path.join(HERE, "libfvc.so")
+OBJDIR = os.path.join(HERE, "build")
+HEADERS = [os.path.join(HERE, "csrc", "fvc_common.h"), os.path.join(os.path.dirname(HERE), "include", "fvc.h")]
+FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Wno-unused-result"]
 
 
-def _stale():
-    if not os.path.exists(OUT):
+def _hipcc():
+    return os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+
+
+def _obj(src):
+    return os.path.join(OBJDIR, os.path.splitext(src)[0] + ".o")
+
+
+def _stale(target, deps):
+    if not os.path.exists(target):
         return True
-    t = os.path.getmtime(OUT)
-    deps = [os.path.join(HERE, "csrc", s) for s in SRCS + ["fvc_common.h"]]
-    deps.append(os.path.join(os.path.dirname(HERE), "include", "fvc.h"))
+    t = os.path.getmtime(target)
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force=False, verbose=True):
-    if not force and not _stale():
-        return OUT
-    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-    cmd = [hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "-shared", "-fPIC",
-           "-Wno-unused-result", "-o", OUT + ".tmp"] + [os.path.join(HERE, "csrc", s) for s in SRCS]
+def _compile(src, verbose):
+    path = os.path.join(HERE, "csrc", src)
+    obj = _obj(src)
+    cmd = [_hipcc()] + FLAGS + ["-c", path, "-o", obj + ".tmp"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
-    os.replace(OUT + ".tmp", OUT)
+    os.replace(obj + ".tmp", obj)
+
+
+def build(force=False, verbose=True):
+    os.makedirs(OBJDIR, exist_ok=True)
+    todo = [s for s in SRCS if force or _stale(_obj(s), [os.path.join(HERE, "csrc", s)] + HEADERS)]
+    if todo:
+        with ThreadPoolExecutor(max_workers=min(len(todo), 4)) as ex:
+            list(ex.map(lambda s: _compile(s, verbose), todo))
+    objs = [_obj(s) for s in SRCS]
+    if force or todo or _stale(OUT, objs):
+        cmd = [_hipcc(), "--offload-arch=gfx950", "-shared", "-fPIC", "-o", OUT + ".tmp"] + objs
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        subprocess.run(cmd, check=True)
+        os.replace(OUT + ".tmp", OUT)
     return OUT
 
 

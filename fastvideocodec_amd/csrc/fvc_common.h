@@ -24,6 +24,20 @@ __device__ __forceinline__ float fvc_apply_in_op(float v, int op) {
   }
 }
 
+// Branch-free form for staging code: selects on a wave-uniform op keep the compiler from
+// splitting the staging path into per-element branches (each with its own s_waitcnt).
+__device__ __forceinline__ float fvc_in_op_sel(float v, int op) {
+  float t = (op == FVC_IN_ROUND) ? rintf(v) : v;
+  t = (op == FVC_IN_ABS) ? fabsf(t) : t;
+  t = (op == FVC_IN_RELU) ? fmaxf(t, 0.f) : t;
+  return t;
+}
+
+__device__ __forceinline__ float4 fvc_in_op_sel4(float4 v, int op) {
+  return make_float4(fvc_in_op_sel(v.x, op), fvc_in_op_sel(v.y, op), fvc_in_op_sel(v.z, op),
+                     fvc_in_op_sel(v.w, op));
+}
+
 __device__ __forceinline__ float4 fvc_apply_in_op4(float4 v, int op) {
   v.x = fvc_apply_in_op(v.x, op);
   v.y = fvc_apply_in_op(v.y, op);

@@ -124,7 +124,7 @@ __global__ __launch_bounds__(kThreads) void conv_mfma_f32_kernel(const ConvArgs 
       float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
       if (iy >= 0 && iy < a.H && ix >= 0 && ix < a.W) {
         v = *reinterpret_cast<const float4*>(xb + ((size_t)iy * a.W + ix) * a.cinp + ch * CC + c4 * 4);
-        v = fvc_apply_in_op4(v, a.in_op);
+        v = fvc_in_op_sel4(v, a.in_op);
       }
       *reinterpret_cast<float4*>(tile + p * CS + c4 * 4) = v;
     }
@@ -231,7 +231,8 @@ __global__ __launch_bounds__(NW * 64) void conv_mfma_pipe_kernel(const ConvArgs 
   extern __shared__ __attribute__((aligned(16))) float smem[];
   int* tap_off = reinterpret_cast<int*>(smem);
   const int tile_floats = (a.ir * a.ic * CS + 3) & ~3;
-  float* tiles[2] = {smem + 64, smem + 64 + tile_floats};
+  float* const tile0 = smem + 64;  // buffers at tile0 and tile0 + tile_floats (no pointer array:
+                                   // it would turn the LDS accesses into flat ones)
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -262,19 +263,17 @@ __global__ __launch_bounds__(NW * 64) void conv_mfma_pipe_kernel(const ConvArgs 
     const int c = p - r * a.ic;
     const int iy = iy0 + r, ix = ix0 + c;
     v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (iy >= 0 && iy < a.H && ix >= 0 && ix < a.W) {
+    if (iy >= 0 && iy < a.H && ix >= 0 && ix < a.W)
       v = *reinterpret_cast<const float4*>(xb + ((size_t)iy * a.W + ix) * a.cinp + ch * CC + c4 * 4);
-      v = fvc_apply_in_op4(v, a.in_op);
-    }
     dst = p * CS + c4 * 4;
-  };
+  };  // in_op is applied at the LDS write (after the MFMAs), see below
 
   // prologue: chunk 0
   for (int e = tid; e < tile_elems; e += NT) {
     float4 v;
     int d;
     fetch(e, 0, v, d);
-    *reinterpret_cast<float4*>(tiles[0] + d) = v;
+    *reinterpret_cast<float4*>(tile0 + d) = fvc_in_op_sel4(v, a.in_op);
   }
 
   f32x16 acc[WM][WN];
@@ -293,8 +292,8 @@ __global__ __launch_bounds__(NW * 64) void conv_mfma_pipe_kernel(const ConvArgs 
   __syncthreads();
 
   for (int ch = 0; ch < a.nchunks; ++ch) {
-    const float* cur = tiles[ch & 1];
-    float* nxt = tiles[(ch + 1) & 1];
+    const float* cur = tile0 + (ch & 1) * tile_floats;
+    float* nxt = tile0 + ((ch + 1) & 1) * tile_floats;
     const bool has_next = ch + 1 < a.nchunks;
     const float* wch = wcls + (size_t)ch * kbc * a.ntp * 128;
     float4 A[WM], Bv[WN], An[WM], Bn[WN];
@@ -334,7 +333,7 @@ __global__ __launch_bounds__(NW * 64) void conv_mfma_pipe_kernel(const ConvArgs 
       for (int m = 0; m < WM; ++m)
 #pragma unroll
         for (int n = 0; n < WN; ++n) acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x2f32(A[m].w, Bv[n].w, acc[m][n], 0, 0, 0);
-      if (sd >= 0) *reinterpret_cast<float4*>(nxt + sd) = sv;
+      if (sd >= 0) *reinterpret_cast<float4*>(nxt + sd) = fvc_in_op_sel4(sv, a.in_op);
 #pragma unroll
       for (int m = 0; m < WM; ++m) A[m] = An[m];
 #pragma unroll
@@ -347,7 +346,7 @@ __global__ __launch_bounds__(NW * 64) void conv_mfma_pipe_kernel(const ConvArgs 
           float4 v;
           int d;
           fetch(e, ch + 1, v, d);
-          *reinterpret_cast<float4*>(nxt + d) = v;
+          *reinterpret_cast<float4*>(nxt + d) = fvc_in_op_sel4(v, a.in_op);
         }
       }
     }
@@ -442,7 +441,7 @@ __global__ __launch_bounds__(kThreads) void deconv2_mfma_f32_kernel(const ConvAr
       float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
       if (iy >= 0 && iy < a.H && ix >= 0 && ix < a.W) {
         v = *reinterpret_cast<const float4*>(xb + ((size_t)iy * a.W + ix) * a.cinp + ch * CC + c4 * 4);
-        v = fvc_apply_in_op4(v, a.in_op);
+        v = fvc_in_op_sel4(v, a.in_op);
       }
       *reinterpret_cast<float4*>(tile + p * CS + c4 * 4) = v;
     }
@@ -571,7 +570,7 @@ __global__ __launch_bounds__(kThreads) void conv_smalln_f32_kernel(const ConvArg
       float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
       if (iy >= 0 && iy < a.H && ix >= 0 && ix < a.W) {
         v = *reinterpret_cast<const float4*>(xb + ((size_t)iy * a.W + ix) * a.cinp + ch * CC + c4 * 4);
-        v = fvc_apply_in_op4(v, a.in_op);
+        v = fvc_in_op_sel4(v, a.in_op);
       }
       *reinterpret_cast<float4*>(tile + p * CS + c4 * 4) = v;
     }
@@ -828,7 +827,7 @@ static int launch_sn_n(int coutp, const ConvArgs& a, dim3 grid, dim3 blk, size_t
 
 template <int CC, int WN, int NW>
 static int launch_pp_t(const ConvArgs& a, dim3 grid, size_t lds, hipStream_t s) {
-  if (lds > 64 * 1024) hipFuncSetAttribute((const void*)conv_mfma_pipe_kernel<CC, 2, WN, NW>,
+  if (lds > 64 * 1024) (void)hipFuncSetAttribute((const void*)conv_mfma_pipe_kernel<CC, 2, WN, NW>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL((conv_mfma_pipe_kernel<CC, 2, WN, NW>), grid, dim3(NW * 64), lds, s, a);
   FVC_CHECK_LAUNCH();

@@ -1,0 +1,658 @@
+// Split-precision implicit-GEMM convolution / transposed convolution on the fp16 matrix cores
+// (v_mfma_f32_32x32x16_f16), at fp32-level accuracy.
+//
+// Replaces the same ATen conv2d / conv_transpose2d calls as fvc_conv.hip (DVC/subnet/
+// endecoder.py:142-169 MEBasic 7x7, :228-296 Warp_net/ResBlock 3x3, analysis_mv.py /
+// synthesis_mv.py 3x3, analysis.py / synthesis.py / prior nets 5x5 s2) for every layer whose
+// padded input channel count is a multiple of 8.
+//
+// Numerics ("fp16 x3"): every fp32 operand v is split exactly as v = hi + lo * 2^-11 with
+// hi = fp16(v), lo = fp16((v - hi) * 2^11) (the residual scaled back into fp16's normal range,
+// so the split keeps ~22 significant bits for any |v| in [6.1e-5, 65504]). Weights are first
+// scaled by a per-layer power of two 2^kw so that max|w| 2^kw lies in [2^13, 2^14). A 32x32 output
+// tile keeps two fp32 accumulators:
+//     main += hi_x * hi_w                       (one MFMA)
+//     corr += hi_x * lo_w + lo_x * hi_w         (two MFMAs)
+// and the epilogue forms (main + corr * 2^-11) * 2^-kw + bias. The omitted lo*lo term is
+// ~2^-22 relative; fp16 products are exact in the fp32 accumulator, so the result tracks an
+// fp32 conv to ~1e-6 relative (tests/test_gpu_kernels.py bounds it like the fp32 kernel).
+// Three fp16 MFMAs (3 x 32 cycles per K=16) replace eight fp32 ones (8 x 64 cycles): 5.3x
+// less matrix time per MAC. An activation with |v| >= 65000 (or NaN) cannot be represented:
+// the staging code raises a device flag (fvc_x3_overflow_flag) instead of silently saturating.
+//
+// Tiling: GEMM M = output pixels (32-pixel strips), N = output channels (32-channel N-tiles),
+// K = taps x input channels walked in k8-blocks = (tap, 8 consecutive channels). One MFMA
+// consumes two k8-blocks: lanes 0-31 hold k8-block 2s, lanes 32-63 hold 2s+1, 8 fp16 each.
+//  * a block = NW waves stacked vertically, each WM strips x WN N-tiles (2 accumulators per
+//    tile); grid = (spatial tiles, N-tile groups, batch x parity classes);
+//  * the input halo tile of one channel chunk (CC channels) is staged in LDS as
+//    [pixel][hi CC | lo CC] fp16 with the pixel stride padded to 16 x odd bytes, so the
+//    ds_read_b128 of 32 strip pixels is conflict-free; stride-2 convs store the tile columns
+//    parity-split (even columns, then odd) so their strips also read consecutive pixels;
+//  * two LDS buffers: while chunk c is multiplied, every thread stages one item of chunk c+1 per
+//    k-step (global load before the MFMAs, split + LDS write after) -> one barrier per chunk;
+//  * weights are pre-split at pack time into [class][chunk][k-step][N-tile][hi|lo][lane] 16-B
+//    fragments, read from L2 straight into VGPRs (1 KB contiguous per wave instruction),
+//    software-pipelined one k-step ahead together with the LDS reads;
+//  * transposed convs: stride^2 output-parity classes, each a stride-1 conv with a tap subset;
+//  * epilogue: scale + bias, ReLU / LeakyReLU(0.1), residual add, exp; pad channels = 0.
+#include "fvc_common.h"
+#include <math.h>
+#include <stdlib.h>
+
+namespace {
+
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+
+constexpr int kMaxTapsX = 49;
+
+__device__ int g_x3_overflow;
+
+struct X3Args {
+  const float* x;
+  const uint4* w;
+  const float* bias;
+  const float* res;
+  float* y;
+  int B, H, W, cinp;
+  int Ho, Wo, coutp, cout;
+  int Hq, Wq;
+  int sin, sout, nclass, nchunks, ntp;
+  int dymin, dxmin, ir, ic, half;  // half > 0: parity-split tile columns (stride-2 conv)
+  int in_op, act, post_op;
+  float osc, osc_c;                // 2^-kw, 2^-kw-11
+  float inv_ic;                    // 1 / ic
+  float act_slope;                 // 0 (ReLU), 0.1 (LeakyReLU), 1 (none)
+  int nks[4];                      // k-steps per chunk, per class
+  int ntaps[4];
+  int oy0[4], ox0[4];
+  long long wcls[4];               // uint4 offset of each class in the pack
+  int toff[4][kMaxTapsX + 1];      // LDS offset (halves) of each tap's window; 0 past ntaps
+};
+
+typedef float f2v __attribute__((ext_vector_type(2)));
+typedef _Float16 h2v __attribute__((ext_vector_type(2)));
+
+template <int IOP>
+__device__ __forceinline__ float in_op_t(float v) {
+  if (IOP == FVC_IN_RELU) return fmaxf(v, 0.f);
+  if (IOP == FVC_IN_ABS) return fabsf(v);
+  if (IOP == FVC_IN_ROUND) return rintf(v);  // torch.round: half-to-even
+  return v;
+}
+
+// v = hi + lo * 2^-11 for 8 values (packed fp16 conversions); mx tracks max |v| for the
+// representability check (|v| < 65000)
+__device__ __forceinline__ void split8(const float (&v)[8], h8& hi, h8& lo, float& mx) {
+#pragma unroll
+  for (int i = 0; i < 8; i += 2) {
+    const f2v x = {v[i], v[i + 1]};
+    const h2v h = __builtin_convertvector(x, h2v);
+    const f2v back = __builtin_convertvector(h, f2v);
+    const h2v l = __builtin_convertvector((x - back) * 2048.f, h2v);
+    hi[i] = h[0];
+    hi[i + 1] = h[1];
+    lo[i] = l[0];
+    lo[i + 1] = l[1];
+  }
+  mx = fmaxf(mx, fmaxf(fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))),
+                       fmaxf(fmaxf(fabsf(v[4]), fabsf(v[5])), fmaxf(fabsf(v[6]), fabsf(v[7])))));
+}
+
+template <int CC, int WM, int WN, int NW, int IOP>
+__global__ __launch_bounds__(NW * 64) void conv_x3_kernel(const X3Args a) {
+  constexpr int C8 = CC / 8;
+  constexpr int PSH = 2 * CC + 8;  // pixel stride in halves: 4*CC bytes + 16 -> 16 x odd bytes
+  constexpr int TH = NW * WM;
+  constexpr int TW = 32;
+  constexpr int NT = NW * 64;
+
+  extern __shared__ __attribute__((aligned(16))) _Float16 smh[];
+  const int tile_h = (a.ir * a.ic * PSH + 7) & ~7;
+  _Float16* const tile0 = smh + 128;  // two buffers at tile0 and tile0 + tile_h (LDS pointers;
+                                      // no pointer array, which would degrade them to flat)
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int li = lane & 31;
+  const int lh = lane >> 5;
+  const int cls = blockIdx.z % a.nclass;
+  const int b = blockIdx.z / a.nclass;
+  const int tiles_x = (a.Wq + TW - 1) / TW;
+  const int ntiles = tiles_x * ((a.Hq + TH - 1) / TH);
+  // persistent over a contiguous run of spatial tiles (row-major: neighbours share halo rows and
+  // columns in this CU's L2); the staging pipeline runs on across tile boundaries
+  const int t_begin = (int)(((long long)ntiles * blockIdx.x) / gridDim.x);
+  const int t_end = (int)(((long long)ntiles * (blockIdx.x + 1)) / gridDim.x);
+  if (t_begin >= t_end) return;
+  const int nt0 = blockIdx.y * WN;
+  const int nq = a.nks[cls];
+  const int hf = a.half;
+  const int nch = a.nchunks;
+  const int tile_items = a.ir * a.ic * C8;
+  const int nstage = (tile_items + NT - 1) / NT;
+  const float* xb = a.x + (size_t)b * a.H * a.W * a.cinp;
+  const uint4* wcls = a.w + a.wcls[cls];
+  float mx = 0.f;  // max |staged value| (fp16 representability check)
+
+  // one staging item = 8 channels of one halo pixel: 2 x float4 global -> hi/lo h8 in LDS.
+  // fetch always issues its two loads (index and coordinates clamped, halo padding selected to 0
+  // in store), so the k-loop has no divergent branches and the compiler can count vmcnt exactly;
+  // in_op, the split and the LDS write happen in store, after the MFMAs.
+  struct Stage {
+    float4 v0, v1;
+    int dst;
+    bool inb;
+  };
+  auto fetch = [&](int e, int tile, int ch, Stage& st) {
+    e = e < tile_items ? e : tile_items - 1;  // duplicates rewrite the same value: benign
+    const int o = e & (C8 - 1);
+    const int p = e / C8;
+    const int r = (int)(((float)p + 0.5f) * a.inv_ic);  // exact: p < 2^14, ic <= 128
+    const int c = p - r * a.ic;
+    const int iy = (tile / tiles_x) * TH * a.sin + a.dymin + r;
+    const int ix = (tile % tiles_x) * TW * a.sin + a.dxmin + c;
+    st.inb = iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
+    const int cy = iy < 0 ? 0 : (iy >= a.H ? a.H - 1 : iy);
+    const int cx = ix < 0 ? 0 : (ix >= a.W ? a.W - 1 : ix);
+    const float* src = xb + ((size_t)cy * a.W + cx) * a.cinp + ch * CC + o * 8;
+    st.v0 = *reinterpret_cast<const float4*>(src);
+    st.v1 = *reinterpret_cast<const float4*>(src + 4);
+    const int cpos = hf ? ((c & 1) * hf + (c >> 1)) : c;
+    st.dst = (r * a.ic + cpos) * PSH + o * 8;
+  };
+  auto store = [&](_Float16* t, const Stage& st) {
+    float v[8] = {st.v0.x, st.v0.y, st.v0.z, st.v0.w, st.v1.x, st.v1.y, st.v1.z, st.v1.w};
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = st.inb ? in_op_t<IOP>(v[i]) : 0.f;
+    h8 hi, lo;
+    split8(v, hi, lo, mx);
+    *reinterpret_cast<h8*>(t + st.dst) = hi;
+    *reinterpret_cast<h8*>(t + st.dst + CC) = lo;
+  };
+
+  for (int e = tid; e < tile_items; e += NT) {
+    Stage st;
+    fetch(e, t_begin, 0, st);
+    store(tile0, st);
+  }
+
+  const int pix0 = (((wave * WM) * a.sin) * a.ic + li) * PSH;  // strip m adds m * pix_m
+  const int pix_m = a.sin * a.ic * PSH;
+  // tap window offsets live one per lane; v_readlane turns them into wave-uniform scalars
+  // without a memory wait inside the k-loop
+  const int tap_tab = a.toff[cls][lane <= kMaxTapsX ? lane : kMaxTapsX];
+  __syncthreads();
+
+  struct Ops {
+    h8 ah[WM], al[WM];
+    uint4 bh[WN], bl[WN];
+  };
+  f32x16 acc[WM][WN], cor[WM][WN];
+  int buf = 0;  // LDS buffer holding the chunk being multiplied
+  for (int tile = t_begin; tile < t_end; ++tile) {
+#pragma unroll
+    for (int m = 0; m < WM; ++m)
+#pragma unroll
+      for (int n = 0; n < WN; ++n)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          acc[m][n][r] = 0.f;
+          cor[m][n][r] = 0.f;
+        }
+
+    // K loop over channel chunks. Two operand register sets (ping-pong, no copies). Each
+    // half-step issues the LDS and global loads of the next k-step (index clamped: the last
+    // prefetch is a harmless repeat) and, in the first k-steps of a chunk, one staging load of
+    // the next chunk (of this tile, or chunk 0 of the next tile); then its MFMAs; then the staging
+    // LDS write. All loads are unconditional and sched_barrier pins the order, so every load has
+    // a full k-step of MFMA work to land behind.
+    for (int ch = 0; ch < nch; ++ch) {
+      const _Float16* cur = tile0 + buf * tile_h;
+      _Float16* nxt = tile0 + (buf ^ 1) * tile_h;
+      const bool last = ch + 1 == nch;
+      const int s_tile = last ? tile + 1 : tile;
+      const int s_ch = last ? 0 : ch + 1;
+      const bool stage_next = s_tile < t_end;
+      const uint4* wch = wcls + (size_t)ch * nq * a.ntp * 128;
+      // k-step q: lane half lh takes k8-block kb = 2q + lh = (tap kb / C8, octet kb % C8)
+      auto load = [&](int q, Ops& op) {
+        int toff;
+        if (C8 == 1) {
+          const int t0 = __builtin_amdgcn_readlane(tap_tab, 2 * q);
+          const int t1 = __builtin_amdgcn_readlane(tap_tab, 2 * q + 1);
+          toff = lh ? t1 : t0;
+        } else {
+          toff = __builtin_amdgcn_readlane(tap_tab, (2 * q) / C8) + (((2 * q) & (C8 - 1)) + lh) * 8;
+        }
+#pragma unroll
+        for (int m = 0; m < WM; ++m) {
+          op.ah[m] = *reinterpret_cast<const h8*>(cur + pix0 + m * pix_m + toff);
+          op.al[m] = *reinterpret_cast<const h8*>(cur + pix0 + m * pix_m + toff + CC);
+        }
+        const uint4* wk = wch + ((size_t)q * a.ntp + nt0) * 128 + lane;
+#pragma unroll
+        for (int n = 0; n < WN; ++n) {
+          op.bh[n] = wk[n * 128];
+          op.bl[n] = wk[n * 128 + 64];
+        }
+      };
+      auto mfmas = [&](const Ops& op) {
+#pragma unroll
+        for (int m = 0; m < WM; ++m)
+#pragma unroll
+          for (int n = 0; n < WN; ++n) {
+            const h8 wh = __builtin_bit_cast(h8, op.bh[n]);
+            const h8 wl = __builtin_bit_cast(h8, op.bl[n]);
+            acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(op.ah[m], wh, acc[m][n], 0, 0, 0);
+            cor[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(op.ah[m], wl, cor[m][n], 0, 0, 0);
+            cor[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(op.al[m], wh, cor[m][n], 0, 0, 0);
+          }
+      };
+      auto half_plain = [&](int q, const Ops& use, Ops& nxt_ops) {
+        load(q + 1 < nq ? q + 1 : nq - 1, nxt_ops);
+        __builtin_amdgcn_sched_barrier(0);
+        mfmas(use);
+        __builtin_amdgcn_sched_barrier(0);
+      };
+      auto half_stage = [&](int q, const Ops& use, Ops& nxt_ops) {
+        load(q + 1 < nq ? q + 1 : nq - 1, nxt_ops);
+        Stage st;
+        fetch(tid + q * NT, s_tile, s_ch, st);
+        __builtin_amdgcn_sched_barrier(0);
+        mfmas(use);
+        __builtin_amdgcn_sched_barrier(0);
+        store(nxt, st);
+      };
+      Ops S0, S1;
+      load(0, S0);
+      const int npair = nq >> 1;
+      const int spair = stage_next ? min((nstage + 1) >> 1, npair) : 0;
+      int q = 0;
+      for (int p = 0; p < spair; ++p, q += 2) {
+        half_stage(q, S0, S1);
+        half_stage(q + 1, S1, S0);
+      }
+      for (int p = spair; p < npair; ++p, q += 2) {
+        half_plain(q, S0, S1);
+        half_plain(q + 1, S1, S0);
+      }
+      if (nq & 1) mfmas(S0);
+      if (stage_next) {
+        for (int qs = 2 * spair; qs < nstage; ++qs) {
+          Stage st;
+          fetch(tid + qs * NT, s_tile, s_ch, st);
+          store(nxt, st);
+        }
+      }
+      __syncthreads();
+      buf ^= 1;
+    }
+
+    // epilogue of this tile (its global stores drain while the next tile's k-loop runs).
+    // Lane (li, lh) holds output channel j = N-tile*32 + li of pixels qx0 + 4lh + {0..3, 8..11,
+    // 16..19, 24..27} (register r -> pixel (r&3) + 8(r>>2) + 4lh). Activation as one max:
+    // relu = max(v, 0*v), lrelu = max(v, 0.1*v), none = max(v, 1*v).
+    const int qy0 = (tile / tiles_x) * TH, qx0 = (tile % tiles_x) * TW;
+    const bool full_w = qx0 + TW <= a.Wq;
+    const int pstride = a.sout * a.coutp;  // output floats per virtual column
+#pragma unroll
+    for (int n = 0; n < WN; ++n) {
+      const int j = (nt0 + n) * 32 + li;
+      const bool real = j < a.cout;
+      const float bj = real ? a.bias[j < a.cout ? j : 0] : 0.f;
+#pragma unroll
+      for (int m = 0; m < WM; ++m) {
+        const int qy = qy0 + wave * WM + m;
+        if (qy >= a.Hq || (nt0 + n) * 32 >= a.coutp) continue;  // wave-uniform
+        const size_t row = (((size_t)b * a.Ho + qy * a.sout + a.oy0[cls]) * a.Wo + a.ox0[cls] +
+                            (size_t)(qx0 + 4 * lh) * a.sout) * a.coutp + j;
+        float* yr = a.y + row;
+        float v[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float t = fmaf(cor[m][n][r], a.osc_c, acc[m][n][r] * a.osc) + bj;
+          v[r] = fmaxf(t, t * a.act_slope);
+        }
+        if (a.res) {
+          const float* rr = a.res + row;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int dx = (r & 3) + 8 * (r >> 2);
+            if (full_w || qx0 + 4 * lh + dx < a.Wq) v[r] += rr[dx * pstride];
+          }
+        }
+        if (a.post_op == FVC_POST_EXP) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) v[r] = expf(v[r]);
+        }
+        if (j < a.coutp) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int dx = (r & 3) + 8 * (r >> 2);
+            if (full_w || qx0 + 4 * lh + dx < a.Wq) yr[dx * pstride] = real ? v[r] : 0.f;
+          }
+        }
+      }
+    }
+  }
+  if (!(mx < 65000.f)) atomicOr(&g_x3_overflow, 1);
+}
+
+// ------------------------------------------------------------------ host-side geometry
+struct X3Cfg {
+  int cinp, coutp, ntp, cc, wm, wn, nw, nclass, nchunks, th, sin, sout;
+  int ntaps[4], nks[4], oy0[4], ox0[4];
+  int tky[4][kMaxTapsX], tkx[4][kMaxTapsX];
+  int tdy[4][kMaxTapsX], tdx[4][kMaxTapsX];
+  int dymin, dymax, dxmin, dxmax;
+  long long wcls[4];
+  long long wtotal;  // uint4 (16-B) units
+};
+
+static int x3_floordiv(int a, int b) { return (a >= 0) ? a / b : -((-a + b - 1) / b); }
+
+static int env_int(const char* n, int dflt) {
+  const char* v = getenv(n);
+  return (v && v[0]) ? atoi(v) : dflt;
+}
+
+// Geometry and tile choice. Returns false for layers the x3 path does not take (cinp % 8 != 0,
+// cout <= 4 -> the VALU small-N kernel, > 128 output channels).
+static bool x3_cfg(int cin, int cout, int ks, int stride, int transposed, X3Cfg& c) {
+  if (cin <= 0 || cout <= 0 || (ks != 1 && ks != 3 && ks != 5 && ks != 7) || (stride != 1 && stride != 2))
+    return false;
+  c.cinp = fvc_rup(cin, 4);
+  c.coutp = fvc_rup(cout, 4);
+  if (c.cinp % 8 || c.coutp <= 4) return false;
+  c.ntp = fvc_cdiv(c.coutp, 32);
+  if (c.ntp > 4) return false;
+  const int pad = ks / 2;
+  if (!transposed) {
+    c.nclass = 1;
+    c.sin = stride;
+    c.sout = 1;
+    c.ntaps[0] = 0;
+    for (int ky = 0; ky < ks; ++ky)
+      for (int kx = 0; kx < ks; ++kx) {
+        const int t = c.ntaps[0]++;
+        c.tky[0][t] = ky; c.tkx[0][t] = kx;
+        c.tdy[0][t] = ky - pad; c.tdx[0][t] = kx - pad;
+      }
+    c.oy0[0] = c.ox0[0] = 0;
+  } else {
+    c.nclass = stride * stride;
+    c.sin = 1;
+    c.sout = stride;
+    for (int py = 0; py < stride; ++py)
+      for (int px = 0; px < stride; ++px) {
+        const int cl = py * stride + px;
+        c.ntaps[cl] = 0;
+        c.oy0[cl] = py; c.ox0[cl] = px;
+        for (int ky = 0; ky < ks; ++ky) {
+          if (((py + pad - ky) % stride + stride) % stride) continue;
+          for (int kx = 0; kx < ks; ++kx) {
+            if (((px + pad - kx) % stride + stride) % stride) continue;
+            const int t = c.ntaps[cl]++;
+            c.tky[cl][t] = ky; c.tkx[cl][t] = kx;
+            c.tdy[cl][t] = x3_floordiv(py + pad - ky, stride);
+            c.tdx[cl][t] = x3_floordiv(px + pad - kx, stride);
+          }
+        }
+      }
+  }
+  c.dymin = c.dxmin = 1 << 20;
+  c.dymax = c.dxmax = -(1 << 20);
+  for (int cl = 0; cl < c.nclass; ++cl)
+    for (int t = 0; t < c.ntaps[cl]; ++t) {
+      c.dymin = c.tdy[cl][t] < c.dymin ? c.tdy[cl][t] : c.dymin;
+      c.dymax = c.tdy[cl][t] > c.dymax ? c.tdy[cl][t] : c.dymax;
+      c.dxmin = c.tdx[cl][t] < c.dxmin ? c.tdx[cl][t] : c.dxmin;
+      c.dxmax = c.tdx[cl][t] > c.dxmax ? c.tdx[cl][t] : c.dxmax;
+    }
+  // channel chunk: the largest of 32 / 16 / 8 dividing cinp (shrunk below if the two LDS tile
+  // buffers do not fit); FVC_X3_CC overrides for experiments
+  c.cc = (c.cinp % 32 == 0) ? 32 : ((c.cinp % 16 == 0) ? 16 : 8);
+  const int want_cc = env_int("FVC_X3_CC", 0);
+  if ((want_cc == 8 || want_cc == 16 || want_cc == 32) && c.cinp % want_cc == 0) c.cc = want_cc;
+  // block shape: 8 waves x 2 strips (16 output rows x 32 columns), 2 waves per SIMD;
+  // FVC_X3_NW / FVC_X3_WM override for experiments (WM=4 only with 4 waves)
+  c.nw = 8;
+  c.wm = env_int("FVC_X3_WM", 2) == 1 ? 1 : 2;
+  // shrink the channel chunk, then the strips per wave, until two tile buffers fit in LDS
+  for (;;) {
+    c.th = c.nw * c.wm;
+    const int ir = (c.th - 1) * c.sin + 1 + (c.dymax - c.dymin);
+    const int ic = 31 * c.sin + 1 + (c.dxmax - c.dxmin);
+    const size_t lds = 256 + 2 * ((((size_t)ir * ic * (2 * c.cc + 8)) + 7) & ~(size_t)7) * 2;
+    if (lds <= 160 * 1024) break;
+    if (c.cc > 8 && c.cinp % (c.cc / 2) == 0) c.cc /= 2;
+    else if (c.wm > 1) c.wm /= 2;
+    else return false;
+  }
+  c.nchunks = c.cinp / c.cc;
+  c.wn = 1;
+  long long off = 0;
+  for (int cl = 0; cl < c.nclass; ++cl) {
+    c.nks[cl] = fvc_cdiv(c.ntaps[cl] * (c.cc / 8), 2);
+    c.wcls[cl] = off;
+    off += (long long)c.nchunks * c.nks[cl] * c.ntp * 128;  // 128 uint4 per (k-step, N-tile)
+  }
+  c.wtotal = off;
+  return true;
+}
+
+static int x3_num_cus() {
+  static int n = 0;
+  if (!n) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+  }
+  return n;
+}
+
+static int x3_kw(const float* w, size_t n) {
+  float mx = 0.f;
+  for (size_t i = 0; i < n; ++i) mx = fabsf(w[i]) > mx ? fabsf(w[i]) : mx;
+  if (!(mx > 0.f) || !isfinite(mx)) return 0;
+  int e;
+  frexpf(mx, &e);  // mx = m * 2^e, m in [0.5, 1)
+  int kw = 14 - e;  // mx * 2^kw in [2^13, 2^14)
+  return kw < -100 ? -100 : (kw > 100 ? 100 : kw);
+}
+
+template <int CC, int WM, int WN, int IOP>
+static int x3_launch_t(const X3Args& a, dim3 grid, size_t lds, hipStream_t s) {
+  if (lds > 64 * 1024)
+    (void)hipFuncSetAttribute((const void*)conv_x3_kernel<CC, WM, WN, 8, IOP>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL((conv_x3_kernel<CC, WM, WN, 8, IOP>), grid, dim3(8 * 64), lds, s, a);
+  FVC_CHECK_LAUNCH();
+  return 0;
+}
+
+template <int CC, int WM, int WN>
+static int x3_launch_iop(int iop, const X3Args& a, dim3 grid, size_t lds, hipStream_t s) {
+  switch (iop) {
+    case FVC_IN_NONE: return x3_launch_t<CC, WM, WN, FVC_IN_NONE>(a, grid, lds, s);
+    case FVC_IN_RELU: return x3_launch_t<CC, WM, WN, FVC_IN_RELU>(a, grid, lds, s);
+    case FVC_IN_ABS: return x3_launch_t<CC, WM, WN, FVC_IN_ABS>(a, grid, lds, s);
+    case FVC_IN_ROUND: return x3_launch_t<CC, WM, WN, FVC_IN_ROUND>(a, grid, lds, s);
+  }
+  return FVC_EINVAL;
+}
+
+// instantiated shapes (8 waves, 2 per SIMD, <= 256 registers: scripts/kres.sh): WM, WN in {1, 2}
+template <int CC>
+static int x3_launch_cc(int wm, int wn, int iop, const X3Args& a, dim3 grid, size_t lds, hipStream_t s) {
+  if (wm == 2 && wn == 2) return x3_launch_iop<CC, 2, 2>(iop, a, grid, lds, s);
+  if (wm == 2 && wn == 1) return x3_launch_iop<CC, 2, 1>(iop, a, grid, lds, s);
+  if (wm == 1 && wn == 2) return x3_launch_iop<CC, 1, 2>(iop, a, grid, lds, s);
+  if (wm == 1 && wn == 1) return x3_launch_iop<CC, 1, 1>(iop, a, grid, lds, s);
+  return FVC_EINVAL;
+}
+
+static int run_x3(const float* x, const void* wpack, float osc, const float* bias, const float* res,
+                  float* y, int batch, int h, int w, int cin, int cout, int ks, int stride, int transposed,
+                  int in_op, int act, int post_op, hipStream_t s) {
+  X3Cfg c;
+  if (!x3_cfg(cin, cout, ks, stride, transposed, c)) return FVC_EINVAL;
+  if (!x || !wpack || !bias || !y || batch <= 0 || h <= 0 || w <= 0) return FVC_EINVAL;
+  X3Args a;
+  a.x = x; a.w = (const uint4*)wpack; a.bias = bias; a.res = res; a.y = y;
+  a.B = batch; a.H = h; a.W = w; a.cinp = c.cinp;
+  a.coutp = c.coutp; a.cout = cout;
+  if (!transposed) {
+    if (stride == 2 && ((h & 1) || (w & 1))) return FVC_EINVAL;
+    a.Ho = h / stride; a.Wo = w / stride;
+    a.Hq = a.Ho; a.Wq = a.Wo;
+  } else {
+    a.Ho = h * stride; a.Wo = w * stride;
+    a.Hq = h; a.Wq = w;
+  }
+  a.sin = c.sin; a.sout = c.sout; a.nclass = c.nclass; a.nchunks = c.nchunks; a.ntp = c.ntp;
+  a.dymin = c.dymin; a.dxmin = c.dxmin;
+  a.ir = (c.th - 1) * c.sin + 1 + (c.dymax - c.dymin);
+  a.ic = 31 * c.sin + 1 + (c.dxmax - c.dxmin);
+  a.half = c.sin == 2 ? (a.ic + 1) / 2 : 0;
+  a.inv_ic = 1.0f / (float)a.ic;
+  a.act_slope = act == FVC_ACT_RELU ? 0.f : (act == FVC_ACT_LRELU ? 0.1f : 1.f);
+  a.in_op = in_op; a.act = act; a.post_op = post_op;
+  a.osc = osc;
+  a.osc_c = osc * (1.0f / 2048.f);
+  for (int cl = 0; cl < 4; ++cl) {
+    const bool v = cl < c.nclass;
+    a.nks[cl] = v ? c.nks[cl] : 0;
+    a.ntaps[cl] = v ? c.ntaps[cl] : 0;
+    a.oy0[cl] = v ? c.oy0[cl] : 0;
+    a.ox0[cl] = v ? c.ox0[cl] : 0;
+    a.wcls[cl] = v ? c.wcls[cl] : 0;
+  }
+  const int psh = 2 * c.cc + 8;
+  for (int cl = 0; cl < 4; ++cl)
+    for (int t = 0; t <= kMaxTapsX; ++t) {
+      int off = 0;
+      if (cl < c.nclass && t < c.ntaps[cl]) {
+        const int cdy = c.tdy[cl][t] - c.dymin;
+        const int cdx = c.tdx[cl][t] - c.dxmin;
+        const int cpos = a.half ? ((cdx & 1) * a.half + (cdx >> 1)) : cdx;
+        off = (cdy * a.ic + cpos) * psh;
+      }
+      a.toff[cl][t] = off;
+    }
+  const size_t tile_h = ((size_t)a.ir * a.ic * psh + 7) & ~(size_t)7;
+  const size_t lds = 256 + 2 * tile_h * 2;
+  if (lds > 160 * 1024) return FVC_EINVAL;
+  const int tiles_x = fvc_cdiv(a.Wq, 32);
+  const int tiles_y = fvc_cdiv(a.Hq, c.th);
+  // N-tiles per block: as many as divide ntp (max 2, or 4 with FVC_X3_WN=4) while the grid
+  // still has >= 1024 blocks to fill 256 CUs
+  int wn = c.ntp >= 2 ? 2 : 1;
+  const int want_wn = env_int("FVC_X3_WN", 0);
+  if (want_wn == 1 || want_wn == 2 || want_wn == 4) wn = want_wn;
+  while (wn > 1 && c.ntp % wn) wn >>= 1;
+  const long long base = (long long)tiles_x * tiles_y * batch * c.nclass;
+  if (!want_wn)
+    while (wn > 1 && base * (c.ntp / wn) < 1024) wn >>= 1;
+  if (wn > 2) wn = 2;
+  // persistent grid: ~one 8-wave block per CU (FVC_X3_BPC blocks per CU), each walking a
+  // contiguous run of spatial tiles
+  const int ncu = x3_num_cus();
+  const long long yz = (long long)(c.ntp / wn) * batch * c.nclass;
+  const int bpc = env_int("FVC_X3_BPC", 1);
+  long long gx = ((long long)ncu * bpc + yz - 1) / yz;
+  if (gx > (long long)tiles_x * tiles_y) gx = (long long)tiles_x * tiles_y;
+  if (gx < 1) gx = 1;
+  dim3 grid((unsigned)gx, c.ntp / wn, batch * c.nclass);
+  switch (c.cc) {
+    case 8: return x3_launch_cc<8>(c.wm, wn, in_op, a, grid, lds, s);
+    case 16: return x3_launch_cc<16>(c.wm, wn, in_op, a, grid, lds, s);
+    case 32: return x3_launch_cc<32>(c.wm, wn, in_op, a, grid, lds, s);
+  }
+  return FVC_EINVAL;
+}
+
+}  // namespace
+
+extern "C" {
+
+int fvc_conv_x3_supported(int cin, int cout, int ksize, int stride, int transposed) {
+  X3Cfg c;
+  return x3_cfg(cin, cout, ksize, stride, transposed, c) ? 1 : 0;
+}
+
+size_t fvc_conv_x3_wpack_bytes(int cin, int cout, int ksize, int stride, int transposed) {
+  X3Cfg c;
+  if (!x3_cfg(cin, cout, ksize, stride, transposed, c)) return 0;
+  return (size_t)c.wtotal * 16;
+}
+
+int fvc_conv_x3_pack_weight(const float* w, void* wp, float* osc_out, int cin, int cout, int ks,
+                            int stride, int transposed) {
+  X3Cfg c;
+  if (!x3_cfg(cin, cout, ks, stride, transposed, c) || !w || !wp || !osc_out) return FVC_EINVAL;
+  const size_t nw = (size_t)cin * cout * ks * ks;
+  const int kw = x3_kw(w, nw);
+  const float sc = ldexpf(1.f, kw);
+  *osc_out = ldexpf(1.f, -kw);
+  _Float16* out = (_Float16*)wp;
+  const int c8n = c.cc / 8;
+  for (long long i = 0; i < c.wtotal * 8; ++i) out[i] = (_Float16)0.f;
+  for (int cl = 0; cl < c.nclass; ++cl)
+    for (int ch = 0; ch < c.nchunks; ++ch)
+      for (int q = 0; q < c.nks[cl]; ++q)
+        for (int nt = 0; nt < c.ntp; ++nt)
+          for (int lane = 0; lane < 64; ++lane) {
+            const int li = lane & 31, lh = lane >> 5;
+            const int kb = 2 * q + lh;
+            const int t = kb / c8n, o = kb % c8n;
+            const int j = nt * 32 + li;
+            if (t >= c.ntaps[cl] || j >= cout) continue;
+            const int ky = c.tky[cl][t], kx = c.tkx[cl][t];
+            const size_t frag = ((((size_t)c.wcls[cl] + (((size_t)ch * c.nks[cl] + q) * c.ntp + nt) * 128)) + lane) * 8;
+            for (int e = 0; e < 8; ++e) {
+              const int ci = ch * c.cc + o * 8 + e;
+              if (ci >= cin) continue;
+              const float v = (transposed ? w[(((size_t)ci * cout + j) * ks + ky) * ks + kx]
+                                          : w[(((size_t)j * cin + ci) * ks + ky) * ks + kx]) * sc;
+              const _Float16 hi = (_Float16)v;
+              const _Float16 lo = (_Float16)((v - (float)hi) * 2048.f);
+              out[frag + e] = hi;              // plane 0 (hi): lanes 0..63
+              out[frag + 64 * 8 + e] = lo;     // plane 1 (lo): +64 lanes
+            }
+          }
+  return 0;
+}
+
+int fvc_conv2d_nhwc_x3(const float* x, const void* wpack, float osc, const float* bias,
+                       const float* res, float* y, int batch, int h, int w, int cin, int cout,
+                       int ksize, int stride, int in_op, int act, int post_op, fvc_stream_t stream) {
+  return run_x3(x, wpack, osc, bias, res, y, batch, h, w, cin, cout, ksize, stride, 0, in_op, act,
+                post_op, (hipStream_t)stream);
+}
+
+int fvc_deconv2d_nhwc_x3(const float* x, const void* wpack, float osc, const float* bias,
+                         const float* res, float* y, int batch, int h, int w, int cin, int cout,
+                         int ksize, int stride, int in_op, int act, int post_op,
+                         fvc_stream_t stream) {
+  return run_x3(x, wpack, osc, bias, res, y, batch, h, w, cin, cout, ksize, stride, 1, in_op, act,
+                post_op, (hipStream_t)stream);
+}
+
+int fvc_x3_overflow_flag(int* host_flag, int reset) {
+  if (!host_flag) return FVC_EINVAL;
+  hipError_t e = hipMemcpyFromSymbol(host_flag, HIP_SYMBOL(g_x3_overflow), sizeof(int), 0,
+                                     hipMemcpyDeviceToHost);
+  if (e != hipSuccess) return -(int)e;
+  if (reset) {
+    const int zero = 0;
+    e = hipMemcpyToSymbol(HIP_SYMBOL(g_x3_overflow), &zero, sizeof(int), 0, hipMemcpyHostToDevice);
+    if (e != hipSuccess) return -(int)e;
+  }
+  return 0;
+}
+
+}  // extern "C"

@@ -132,23 +132,46 @@ def gdn(x, beta, gamma, inverse):
 
 
 # ------------------------------------------------------------------ conv
+def conv_precision() -> str:
+    """'x3' (default): split-precision fp16 matrix-core kernel (fvc_conv_x3.hip) wherever the
+    layer supports it; 'f32': the fp32-MFMA kernel everywhere (FVC_CONV_PRECISION=f32)."""
+    import os
+    p = os.environ.get("FVC_CONV_PRECISION", "x3")
+    if p not in ("x3", "f32"):
+        raise ValueError(f"FVC_CONV_PRECISION must be x3 or f32, got {p!r}")
+    return p
+
+
 class PackedConv:
-    """A conv / transposed conv with weights packed for the MFMA kernel."""
+    """A conv / transposed conv with weights packed once for its HIP kernel: the split-precision
+    fp16 x3 kernel where supported (cin padded to a multiple of 8, cout > 4), else fp32 MFMA /
+    the small-N VALU kernel."""
 
     def __init__(self, weight: torch.Tensor, bias: torch.Tensor, ksize: int, stride: int, transposed: bool,
-                 device):
+                 device, precision: str | None = None):
+        import ctypes
         lib = _lib.load()
         w = weight.detach().to("cpu", torch.float32).contiguous()
         if transposed:
             cin, cout = w.shape[0], w.shape[1]
         else:
             cout, cin = w.shape[0], w.shape[1]
-        n = lib.fvc_conv_wpack_floats(cin, cout, ksize, stride, int(transposed))
-        if n == 0:
-            raise ValueError(f"unsupported conv geometry cin={cin} cout={cout} k={ksize} s={stride}")
-        packed = torch.empty(n, dtype=torch.float32)
-        _lib.call("fvc_conv_pack_weight", w.data_ptr(), packed.data_ptr(), cin, cout, ksize, stride,
-                  int(transposed))
+        precision = precision or conv_precision()
+        self.x3 = precision == "x3" and bool(lib.fvc_conv_x3_supported(cin, cout, ksize, stride, int(transposed)))
+        if self.x3:
+            nbytes = lib.fvc_conv_x3_wpack_bytes(cin, cout, ksize, stride, int(transposed))
+            packed = torch.empty(nbytes // 2, dtype=torch.float16)
+            osc = ctypes.c_float(0.0)
+            _lib.call("fvc_conv_x3_pack_weight", w.data_ptr(), packed.data_ptr(), ctypes.addressof(osc), cin, cout,
+                      ksize, stride, int(transposed))
+            self.osc = float(osc.value)
+        else:
+            n = lib.fvc_conv_wpack_floats(cin, cout, ksize, stride, int(transposed))
+            if n == 0:
+                raise ValueError(f"unsupported conv geometry cin={cin} cout={cout} k={ksize} s={stride}")
+            packed = torch.empty(n, dtype=torch.float32)
+            _lib.call("fvc_conv_pack_weight", w.data_ptr(), packed.data_ptr(), cin, cout, ksize, stride,
+                      int(transposed))
         self.wpack = packed.to(device)
         self.bias = bias.detach().to(device, torch.float32).contiguous()
         self.cin, self.cout, self.ksize, self.stride, self.transposed = cin, cout, ksize, stride, transposed
@@ -170,20 +193,35 @@ class PackedConv:
         _chk(res, oshape, name="res")
         y = out if out is not None else torch.empty(oshape, dtype=torch.float32, device=x.device)
         _chk(y, oshape, name="y")
-        fn = "fvc_deconv2d_nhwc_f32" if self.transposed else "fvc_conv2d_nhwc_f32"
         timer = profiling.active()
         if timer is not None:
             ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             ev0.record()
-        _lib.call(fn, x.data_ptr(), self.wpack.data_ptr(), self.bias.data_ptr(), _ptr(res), y.data_ptr(), B, H, W,
-                  self.cin, self.cout, self.ksize, self.stride, in_op, act, post, stream_handle())
+        if self.x3:
+            fn = "fvc_deconv2d_nhwc_x3" if self.transposed else "fvc_conv2d_nhwc_x3"
+            _lib.call(fn, x.data_ptr(), self.wpack.data_ptr(), self.osc, self.bias.data_ptr(), _ptr(res),
+                      y.data_ptr(), B, H, W, self.cin, self.cout, self.ksize, self.stride, in_op, act, post,
+                      stream_handle())
+        else:
+            fn = "fvc_deconv2d_nhwc_f32" if self.transposed else "fvc_conv2d_nhwc_f32"
+            _lib.call(fn, x.data_ptr(), self.wpack.data_ptr(), self.bias.data_ptr(), _ptr(res), y.data_ptr(), B, H,
+                      W, self.cin, self.cout, self.ksize, self.stride, in_op, act, post, stream_handle())
         if timer is not None:
             ev1.record()
             timer.records.append((ev0, ev1, profiling.conv_flops(self.cin, self.cout, self.ksize, self.stride,
                                                                  self.transposed, B, H, W),
                                   f"{'deconv' if self.transposed else 'conv'}{self.ksize}s{self.stride} "
-                                  f"{self.cin}->{self.cout} @{H}x{W}"))
+                                  f"{self.cin}->{self.cout} @{H}x{W}{' x3' if self.x3 else ''}"))
         return y
+
+
+def x3_overflow(reset: bool = True) -> bool:
+    """True if any split-precision conv staged an activation with |v| >= 65000 since the last
+    reset (synchronises the device)."""
+    import ctypes
+    flag = ctypes.c_int(0)
+    _lib.call("fvc_x3_overflow_flag", ctypes.addressof(flag), int(reset))
+    return bool(flag.value)
 
 
 # ------------------------------------------------------------------ reductions

@@ -72,6 +72,27 @@ int fvc_deconv2d_nhwc_f32(const float* x, const float* wpack, const float* bias,
                           int ksize, int stride, int in_op, int act, int post_op,
                           fvc_stream_t stream);
 
+/* Split-precision variant ("fp16 x3", fvc_conv_x3.hip): same math and arguments, computed on the
+ * fp16 matrix cores with every fp32 operand split into hi + lo*2^-11 halves and three MFMAs per
+ * product (fp32-level accuracy, ~1e-6 relative). Taken for layers with cin padded to a multiple
+ * of 8 and cout > 4 (fvc_conv_x3_supported). The pack is fp16 pairs plus a per-layer output
+ * scale osc = 2^-kw (weights are pre-scaled by 2^kw). Activations must stay below 65000 in
+ * magnitude: staging raises a device flag otherwise, read (and optionally reset) with
+ * fvc_x3_overflow_flag (synchronous). */
+int fvc_conv_x3_supported(int cin, int cout, int ksize, int stride, int transposed);
+size_t fvc_conv_x3_wpack_bytes(int cin, int cout, int ksize, int stride, int transposed);
+int fvc_conv_x3_pack_weight(const float* w_host, void* wpack_host, float* osc_out, int cin,
+                            int cout, int ksize, int stride, int transposed);
+int fvc_conv2d_nhwc_x3(const float* x, const void* wpack, float osc, const float* bias,
+                       const float* res, float* y, int batch, int h, int w, int cin, int cout,
+                       int ksize, int stride, int in_op, int act, int post_op,
+                       fvc_stream_t stream);
+int fvc_deconv2d_nhwc_x3(const float* x, const void* wpack, float osc, const float* bias,
+                         const float* res, float* y, int batch, int h, int w, int cin, int cout,
+                         int ksize, int stride, int in_op, int act, int post_op,
+                         fvc_stream_t stream);
+int fvc_x3_overflow_flag(int* host_flag, int reset);
+
 /* ------------------------------------------------------------------ layout / resampling */
 int fvc_nchw_to_nhwc(const float* src, float* dst, int batch, int c, int h, int w, int cp,
                      fvc_stream_t stream);

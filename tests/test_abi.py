@@ -73,3 +73,38 @@ def test_state_dict_matches_reference_layout():
     assert list(own.keys()) == list(sd.keys())
     for k, v in sd.items():
         assert tuple(own[k].shape) == v.shape, k
+
+
+@pytest.mark.parametrize("geom", [(8, 32, 7, 1, 0), (32, 64, 7, 1, 0), (64, 64, 3, 1, 0), (128, 128, 3, 2, 1),
+                                  (128, 128, 3, 2, 0), (96, 64, 5, 2, 1), (64, 96, 3, 1, 1), (6, 64, 3, 1, 0)])
+def test_x3_pack_splits_every_weight_once(geom):
+    """Split-precision pack (fvc_conv_x3.hip): every weight appears exactly once as a hi/lo fp16
+    pair with hi + lo*2^-11 == w*2^kw to ~2^-22 relative, and max|w|*2^kw lies in [2^13, 2^14)."""
+    import ctypes
+    lib = _lib.load()
+    cin, cout, k, s, tr = geom
+    assert lib.fvc_conv_x3_supported(*geom) == 1
+    nbytes = lib.fvc_conv_x3_wpack_bytes(*geom)
+    assert nbytes > 0 and nbytes % 2048 == 0
+    g = torch.Generator().manual_seed(sum(geom))
+    w = torch.randn((cin, cout, k, k) if tr else (cout, cin, k, k), generator=g) * 0.03
+    out = torch.empty(nbytes // 2, dtype=torch.float16)
+    osc = ctypes.c_float(0)
+    assert lib.fvc_conv_x3_pack_weight(w.data_ptr(), out.data_ptr(), ctypes.addressof(osc), cin, cout, k, s, tr) == 0
+    frags = out.view(-1, 2, 64, 8).double()  # [k-step x N-tile][hi|lo][lane][8]
+    val = (frags[:, 0] + frags[:, 1] * 2.0 ** -11).flatten()
+    hi = frags[:, 0].flatten()
+    nz = hi != 0
+    assert int(nz.sum()) == w.numel()
+    rec = torch.sort(val[nz] * osc.value).values
+    ref = torch.sort(w.flatten().double()).values
+    assert torch.allclose(rec, ref, rtol=2 ** -20, atol=0)
+    scaled = float(w.abs().max()) / osc.value
+    assert 2 ** 13 <= scaled < 2 ** 14
+
+
+def test_x3_rejects_unsupported_layers():
+    lib = _lib.load()
+    assert lib.fvc_conv_x3_supported(2, 128, 3, 2, 0) == 0  # cin padded to 4: fp32 kernel
+    assert lib.fvc_conv_x3_supported(64, 3, 3, 1, 0) == 0   # cout <= 4: VALU small-N kernel
+    assert lib.fvc_conv_x3_wpack_bytes(64, 3, 3, 1, 0) == 0

@@ -61,8 +61,9 @@ def _in_op(x, op):
     return {K.IN_NONE: x, K.IN_RELU: F.relu(x), K.IN_ABS: x.abs(), K.IN_ROUND: torch.round(x)}[op]
 
 
+@pytest.mark.parametrize("precision", ["x3", "f32"])
 @pytest.mark.parametrize("case", CONV_CASES, ids=lambda c: f"ci{c[0]}co{c[1]}k{c[2]}s{c[3]}{'T' if c[4] else ''}")
-def test_conv(dev, case):
+def test_conv(dev, case, precision):
     cin, cout, k, s, tr, H, W, in_op, act, post, with_res = case
     g = torch.Generator().manual_seed(cin * 1000 + cout + k)
     x = torch.randn(2, cin, H, W, generator=g) * 2.0
@@ -83,15 +84,49 @@ def test_conv(dev, case):
         ref = ref + res
     if post == K.POST_EXP:
         ref = torch.exp(ref)
-    pc = K.PackedConv(w, b, k, s, tr, dev)
+    pc = K.PackedConv(w, b, k, s, tr, dev, precision=precision)
+    K.x3_overflow(reset=True)
     y = pc(to_nhwc(x).to(dev), in_op=in_op, act=act, post=post,
            res=None if res is None else to_nhwc(res).to(dev))
     torch.cuda.synchronize()
+    assert not K.x3_overflow(reset=True)
     yc = y.cpu()
     assert yc.shape[1:3] == ref.shape[2:]
     close(from_nhwc(yc, cout), ref, 2e-5)
     if K.cp4(cout) > cout:
         assert float(yc[..., cout:].abs().max()) == 0.0, "pad channels must be zero"
+
+
+def test_conv_x3_overflow_flag(dev):
+    """|activation| >= 65000 cannot be split into fp16 halves: the x3 kernel must flag it."""
+    w = torch.randn(64, 64, 3, 3) * 0.05
+    pc = K.PackedConv(w, torch.zeros(64), 3, 1, False, dev, precision="x3")
+    assert pc.x3
+    x = torch.zeros(1, 64, 16, 32)
+    K.x3_overflow(reset=True)
+    pc(to_nhwc(x).to(dev))
+    assert not K.x3_overflow(reset=True)
+    x[0, 5, 3, 7] = 7.0e4
+    pc(to_nhwc(x).to(dev))
+    assert K.x3_overflow(reset=True)
+
+
+def test_conv_x3_matches_f32_closely(dev):
+    """The split-precision kernel tracks the fp32 MFMA kernel to ~1e-6 relative on a 3x3 64-ch
+    layer at a realistic activation scale (ulp-level differences only)."""
+    g = torch.Generator().manual_seed(11)
+    x = torch.rand(1, 64, 48, 96, generator=g) * 3.0
+    w = torch.randn(64, 64, 3, 3, generator=g) * 0.04
+    b = torch.randn(64, generator=g) * 0.1
+    ref = F.conv2d(x.double(), w.double(), b.double(), 1, 1).float()
+    xd = to_nhwc(x).to(dev)
+    y3 = K.PackedConv(w, b, 3, 1, False, dev, precision="x3")(xd)
+    y32 = K.PackedConv(w, b, 3, 1, False, dev, precision="f32")(xd)
+    torch.cuda.synchronize()
+    e3 = float((from_nhwc(y3.cpu(), 64) - ref).abs().max())
+    e32 = float((from_nhwc(y32.cpu(), 64) - ref).abs().max())
+    scale = float(ref.abs().max())
+    assert e3 <= 4e-6 * scale, (e3, e32, scale)
 
 
 def test_conv_deterministic(dev):
