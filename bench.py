@@ -31,6 +31,7 @@ from fastvideocodec_amd.gop import encode_decode_gop  # noqa: E402
 from fastvideocodec_amd.models import get_codec_model  # noqa: E402
 from fastvideocodec_amd.synthetic import gop_seed, make_gop  # noqa: E402
 
+F16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16/F16 dense matrix peak (~2.5 PF)
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 matrix (v_mfma_f32_32x32x2_f32), dense
 ENC_TFLOP_PER_PFRAME = 2.931   # SURVEY.md §8(d) algorithmic, 1920x1088
 DEC_TFLOP_PER_PFRAME = 1.295
@@ -121,14 +122,18 @@ def main():
     with timer:
         encode_decode_gop(model, frames, overlap=False)
     conv_ms, conv_flops, n_launch = timer.collect()
+    x3_ms, x3_flops, x3_launch = timer.collect(x3=True)
     if args.breakdown and rank == 0:
         agg = timer.breakdown()
         for k, (n, ms, fl) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
             print(f"{k:40s} n={n:5d} ms={ms:9.2f} TF/s={fl / (ms * 1e-3) / 1e12:7.2f}", file=sys.stderr)
 
     # ---- verification + quality, outside the timed region
+    from fastvideocodec_amd import kernels as K
+    K.x3_overflow(reset=True)
     bss, decoded, sses, encs = encode_decode_gop(model, frames, check=True)
     torch.cuda.synchronize()
+    x3_overflow = K.x3_overflow(reset=True)
     bitexact = all(torch.equal(a, b) for a, b in zip(decoded, encs))
     nbytes = sum(b.nbytes() for b in bss)
     npx = G * 3 * Hp * Wp
@@ -147,7 +152,8 @@ def main():
 
     pframes = args.steps * G * (args.gop - 1) * world
     value = pframes / dt_max
-    achieved = conv_flops / (conv_ms * 1e-3) / 1e12 if conv_ms > 0 else 0.0
+    nfr = G * (args.gop - 1)
+    achieved = x3_flops / (x3_ms * 1e-3) / 1e12 if x3_ms > 0 else 0.0
     result = {
         "metric": "1080p frames/sec encode+decode at λ=1024; bpp/PSNR parity vs CPU ref",
         "value": round(value, 3),
@@ -159,21 +165,30 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32",
+        "dtype": "f32 (convs: fp32 operands split into fp16 hi/lo, f32 accumulate)",
         "data": "synthetic (seeded GOP generator, SURVEY.md §8(d)); seeded weights + pretrained SpyNet",
         "config": {"workload": f"DVC P-frame encode+decode with rANS, {args.width}x{args.height} "
                                f"(padded {Wp}x{Hp}) GOP-{args.gop}, lambda=1024 slot",
                    "gops_per_gpu": G, "frames_counted": "P-frames only (I-frame pass-through)",
                    "parallelism": f"gop-shard x{world}"},
-        "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_MFMA_PEAK_TFLOPS,
-                     "unit": "TFLOP/s", "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
-                     "kernel": "conv family (conv_mfma_f32 / pipe / deconv2 / smalln): all conv+deconv launches",
+        "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": F16_MFMA_PEAK_TFLOPS,
+                     "unit": "TFLOP/s", "frac": round(achieved / F16_MFMA_PEAK_TFLOPS, 4), "traffic": None,
+                     "kernel": "conv_x3_kernel (split-precision fp16x3 implicit-GEMM conv/deconv): all its launches",
+                     "achieved_is": "algorithmic fp32-conv FLOP (2 x MAC) / kernel time; the kernel issues 3 f16 "
+                                    "MFMAs per MAC, so its ceiling in these units is peak/3",
+                     "x3_ceiling": round(F16_MFMA_PEAK_TFLOPS / 3, 1),
+                     "frac_of_x3_ceiling": round(achieved / (F16_MFMA_PEAK_TFLOPS / 3), 4),
                      "measured": "HIP events on the launching stream around every conv launch of one serial GOP",
-                     "launches": n_launch, "conv_ms_per_pframe": round(conv_ms / (G * (args.gop - 1)), 3),
-                     "conv_gflop_per_pframe": round(conv_flops / (G * (args.gop - 1)) / 1e9, 1)},
+                     "launches": x3_launch, "ms_per_pframe": round(x3_ms / nfr, 3),
+                     "gflop_per_pframe": round(x3_flops / nfr / 1e9, 1),
+                     "all_convs": {"ms_per_pframe": round(conv_ms / nfr, 3),
+                                   "gflop_per_pframe": round(conv_flops / nfr / 1e9, 1),
+                                   "tflops": round(conv_flops / (conv_ms * 1e-3) / 1e12, 2) if conv_ms else 0.0,
+                                   "launches": n_launch}},
         "quality": {"decoder_bitexact": bitexact_all, "bytes_per_pframe": round(bytes_all / (G * (args.gop - 1) * world), 1),
                     "bpp_actual": round(bytes_all * 8 / (G * (args.gop - 1) * world * Hp * Wp), 5),
-                    "psnr_db_mean": round(psnr_all, 4)},
+                    "psnr_db_mean": round(psnr_all, 4),
+                    "x3_operand_overflow": x3_overflow},
         "model_tflop_per_pframe": ENC_TFLOP_PER_PFRAME + DEC_TFLOP_PER_PFRAME,
     }
     result["effective_tflops"] = round(value / world * (ENC_TFLOP_PER_PFRAME + DEC_TFLOP_PER_PFRAME), 2)

@@ -50,10 +50,10 @@ _SIGS = {
     "fvc_pmf_to_quantized_cdf": (c_int, [vp, c_int, c_int, vp]),
     "fvc_rans_encode_ws_bytes": (c_size_t, [ctypes.c_int64]),
     "fvc_rans_encode": (c_int, [vp, vp, vp, c_int, ctypes.c_int64, vp, c_int, vp, vp, vp, vp, vp, vp, vp]),
-    "fvc_rans_lut_bytes": (c_size_t, [c_int]),
+    "fvc_rans_lut_bytes": (c_size_t, [c_int, c_int]),
     "fvc_rans_build_lut": (c_int, [vp, c_int, vp, c_int, vp, vp]),
     "fvc_rans_pack": (c_int, [vp, vp, vp, c_int, vp, vp, vp]),
-    "fvc_rans_decode": (c_int, [vp, vp, vp, vp, c_int, c_int, vp, vp, vp, vp, vp, vp]),
+    "fvc_rans_decode": (c_int, [vp, vp, vp, vp, c_int, c_int, c_int, vp, vp, vp, vp, vp, vp]),
 }
 
 EXPORTED = tuple(_SIGS)

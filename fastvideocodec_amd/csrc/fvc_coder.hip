@@ -130,6 +130,10 @@ __device__ __forceinline__ uint64_t mulhi64(uint64_t a, uint64_t b) { return __u
 
 // Phase 2: one lane per stream walks its symbols backward (compressai's BufferedRansEncoder
 // pushes forward and flushes backward; each symbol's sub-symbols are put in reverse push order).
+// The per-symbol records are independent of the state chain, so they are fetched kPf ahead in
+// register blocks: the chain then runs at ALU latency instead of one memory latency per symbol.
+constexpr int kPf = 8;
+
 __global__ void k_rans_encode(const EncSym* __restrict__ prep, const uint32_t* __restrict__ raw_in,
                               const int64_t* __restrict__ sym_off, int nstreams, uint32_t* __restrict__ words,
                               const int64_t* __restrict__ word_off, int32_t* __restrict__ nwords) {
@@ -141,33 +145,48 @@ __global__ void k_rans_encode(const EncSym* __restrict__ prep, const uint32_t* _
   uint64_t x = kRansL;
   bool ok = true;
   const int64_t b = sym_off[s];
-  int64_t i = sym_off[s + 1] - 1;
-  EncSym pnext;
-  if (i >= b) pnext = prep[i];
-  for (; ok && i >= b; --i) {
-    const EncSym p = pnext;
-    if (i > b) pnext = prep[i - 1];  // prefetch: independent of the state chain
-    const uint32_t start = p.sf & 0xFFFFu, freq = p.sf >> 16;
-    if (p.shift & 0x100u) {  // escape bin: bypass-coded payload
-      const uint32_t raw = raw_in[i];
-      int32_t nb = 0;
-      while (nb < 8 && (raw >> (nb * kBypassPrec)) != 0) ++nb;
-      for (int32_t j = nb - 1; ok && j >= 0; --j) ok = enc_put_bits(x, ptr, lo, (raw >> (j * kBypassPrec)) & kMaxBypass);
-      const int32_t q = nb / kMaxBypass, r = nb - q * kMaxBypass;
-      if (ok) ok = enc_put_bits(x, ptr, lo, (uint32_t)r);
-      for (int32_t k = 0; ok && k < q; ++k) ok = enc_put_bits(x, ptr, lo, kMaxBypass);
-      if (!ok) break;
+  EncSym cur[kPf], nxt[kPf];
+  int64_t i = sym_off[s + 1] - 1;  // symbol index of cur[0]; cur[k] = prep[i - k]
+#pragma unroll
+  for (int k = 0; k < kPf; ++k)
+    if (i - k >= b) cur[k] = prep[i - k];
+  for (; ok && i >= b; i -= kPf) {
+#pragma unroll
+    for (int k = 0; k < kPf; ++k)
+      if (i - kPf - k >= b) nxt[k] = prep[i - kPf - k];
+#pragma unroll
+    for (int k = 0; k < kPf; ++k) {
+      const int64_t ik = i - k;
+      if (!ok || ik < b) break;
+      const EncSym p = cur[k];
+      const uint32_t start = p.sf & 0xFFFFu, freq = p.sf >> 16;
+      if (p.shift & 0x100u) {  // escape bin: bypass-coded payload
+        const uint32_t raw = raw_in[ik];
+        int32_t nb = 0;
+        while (nb < 8 && (raw >> (nb * kBypassPrec)) != 0) ++nb;
+        for (int32_t j = nb - 1; ok && j >= 0; --j)
+          ok = enc_put_bits(x, ptr, lo, (raw >> (j * kBypassPrec)) & kMaxBypass);
+        const int32_t q = nb / kMaxBypass, r = nb - q * kMaxBypass;
+        if (ok) ok = enc_put_bits(x, ptr, lo, (uint32_t)r);
+        for (int32_t kk = 0; ok && kk < q; ++kk) ok = enc_put_bits(x, ptr, lo, kMaxBypass);
+        if (!ok) break;
+      }
+      const uint64_t x_max = ((kRansL >> kPrec) << 32) * freq;
+      if (x >= x_max) {
+        if (ptr <= lo) {
+          ok = false;
+          break;
+        }
+        *--ptr = (uint32_t)x;
+        x >>= 32;
+      }
+      // Rans64EncPutSymbol: x = x + bias + q * (2^prec - freq), q = mulhi(x, rcp) >> shift
+      const uint64_t q = mulhi64(x, p.rcp) >> (p.shift & 0xFFu);
+      const uint64_t bias = freq < 2 ? (uint64_t)start + (1u << kPrec) - 1 : (uint64_t)start;
+      x = x + bias + q * (uint64_t)((1u << kPrec) - freq);
     }
-    const uint64_t x_max = ((kRansL >> kPrec) << 32) * freq;
-    if (x >= x_max) {
-      if (ptr <= lo) { ok = false; break; }
-      *--ptr = (uint32_t)x;
-      x >>= 32;
-    }
-    // Rans64EncPutSymbol: x = x + bias + q * (2^prec - freq), q = mulhi(x, rcp) >> shift
-    const uint64_t q = mulhi64(x, p.rcp) >> (p.shift & 0xFFu);
-    const uint64_t bias = freq < 2 ? (uint64_t)start + (1u << kPrec) - 1 : (uint64_t)start;
-    x = x + bias + q * (uint64_t)((1u << kPrec) - freq);
+#pragma unroll
+    for (int k = 0; k < kPf; ++k) cur[k] = nxt[k];
   }
   if (ok && ptr - lo >= 2) {
     ptr -= 2;
@@ -217,40 +236,49 @@ __global__ void k_pack_copy(const uint32_t* __restrict__ words, const int64_t* _
 }
 
 
-// Decode LUTs: lut[t][cum] = the symbol s of table t with cdf[s] <= cum < cdf[s+1], and
-// lutsf[t][cum] = cdf[s] | (cdf[s+1]-cdf[s]) << 16. The state update needs only lutsf, so each
-// decoded symbol costs one dependent load (lut, needed only for the output value, is issued in
-// parallel and is off the state chain).
+// Decode tables, small enough to stay L2-resident: per table t
+//   lut[t][u]  (u = cum >> kLutShift, 4096 buckets): the symbol s with cdf[s] <= u << kLutShift
+//              < cdf[s+1], i.e. the first candidate for any cum in that bucket;
+//   sf[t][s]   = cdf[s] | (cdf[s+1] - cdf[s]) << 16.
+// A decoded symbol costs two dependent L2 hits (bucket, then its start/freq) plus a short
+// forward step when the bucket straddles a symbol boundary; the old 2^16-entry LUT was one
+// random access into 256 KB per table, missing in L2 almost every time.
+constexpr int kLutShift = 4;
+constexpr int kLutN = 1 << (kPrec - kLutShift);
+
 __global__ void k_build_lut(const int32_t* __restrict__ cdfs, int cdf_stride, const int32_t* __restrict__ cdf_sizes,
-                            int ntables, uint16_t* __restrict__ lut, uint32_t* __restrict__ lutsf) {
-  const int64_t n = (int64_t)ntables << kPrec;
-  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
-    const int t = (int)(e >> kPrec);
-    const uint32_t cum = (uint32_t)(e & ((1 << kPrec) - 1));
-    const int32_t* cdf = cdfs + (size_t)t * cdf_stride;
-    int lo = 0, hi = cdf_sizes[t] - 1;
-    while (hi - lo > 1) {
-      const int mid = (lo + hi) >> 1;
-      if ((uint32_t)cdf[mid] <= cum) lo = mid; else hi = mid;
+                            int ntables, uint16_t* __restrict__ lut, uint32_t* __restrict__ sf) {
+  const int64_t nl = (int64_t)ntables * kLutN;
+  const int64_t ns = (int64_t)ntables * cdf_stride;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < nl + ns; e += (int64_t)gridDim.x * blockDim.x) {
+    if (e < nl) {
+      const int t = (int)(e / kLutN);
+      const uint32_t cum = (uint32_t)(e % kLutN) << kLutShift;
+      const int32_t* cdf = cdfs + (size_t)t * cdf_stride;
+      int lo = 0, hi = cdf_sizes[t] - 1;
+      while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if ((uint32_t)cdf[mid] <= cum) lo = mid; else hi = mid;
+      }
+      lut[e] = (uint16_t)lo;
+    } else {
+      const int64_t f = e - nl;
+      const int t = (int)(f / cdf_stride);
+      const int sidx = (int)(f % cdf_stride);
+      const int32_t* cdf = cdfs + (size_t)t * cdf_stride;
+      sf[f] = sidx < cdf_sizes[t] - 1 ? ((uint32_t)cdf[sidx] | ((uint32_t)(cdf[sidx + 1] - cdf[sidx]) << 16)) : 0u;
     }
-    lut[e] = (uint16_t)lo;
-    lutsf[e] = (uint32_t)cdf[lo] | ((uint32_t)(cdf[lo + 1] - cdf[lo]) << 16);
   }
 }
 
-__device__ __forceinline__ bool dec_renorm(uint64_t& x, const uint32_t*& ptr, const uint32_t* end) {
-  if (x < kRansL) {
-    if (ptr >= end) return false;
-    x = (x << 32) | *ptr++;
-  }
-  return true;
-}
-
+// One lane per stream. The next bitstream word and the next kPf table indexes are held in
+// registers ahead of need, so the only memory accesses on the state chain are the two table hits.
 __global__ void k_rans_decode(const uint32_t* __restrict__ packed, const int64_t* __restrict__ pack_off,
                               const int32_t* __restrict__ indexes, const int64_t* __restrict__ sym_off, int nstreams,
-                              const int32_t* __restrict__ cdf_sizes, const int32_t* __restrict__ offsets,
-                              const uint16_t* __restrict__ lut, const uint32_t* __restrict__ lutsf,
-                              int32_t* __restrict__ symbols, int32_t* __restrict__ status) {
+                              int cdf_stride, const int32_t* __restrict__ cdf_sizes,
+                              const int32_t* __restrict__ offsets, const uint16_t* __restrict__ lut,
+                              const uint32_t* __restrict__ sft, int32_t* __restrict__ symbols,
+                              int32_t* __restrict__ status) {
   const int s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= nstreams) return;
   const uint32_t* ptr = packed + pack_off[s];
@@ -261,50 +289,71 @@ __global__ void k_rans_decode(const uint32_t* __restrict__ packed, const int64_t
     x = (uint64_t)ptr[0] | ((uint64_t)ptr[1] << 32);
     ptr += 2;
   }
+  uint32_t wnext = ptr < end ? *ptr : 0u;  // next renormalisation word, loaded ahead
+  auto renorm = [&]() {
+    if (x < kRansL) {
+      if (ptr >= end) return false;
+      x = (x << 32) | wnext;
+      ++ptr;
+      wnext = ptr < end ? *ptr : 0u;
+    }
+    return true;
+  };
   const uint64_t mask = (1ull << kPrec) - 1;
   const int64_t e = sym_off[s + 1];
   int64_t i = sym_off[s];
-  int32_t cnext = i < e ? indexes[i] : 0;
-  for (; i < e; ++i) {
-    const int32_t ci = cnext;
-    if (i + 1 < e) cnext = indexes[i + 1];  // prefetch: independent of the state chain
-    if (!ok) {
-      symbols[i] = 0;
-      continue;
-    }
-    const uint32_t cum = (uint32_t)(x & mask);
-    const size_t li = ((size_t)ci << kPrec) | cum;
-    const uint32_t sf = lutsf[li];
-    const int32_t sidx = lut[li];
-    const uint32_t start = sf & 0xFFFFu, freq = sf >> 16;
-    x = freq * (x >> kPrec) + cum - start;
-    ok = dec_renorm(x, ptr, end);
-    int32_t value = sidx;
-    if (ok && start + freq == (1u << kPrec)) {  // escape bin (== max_value)
-      auto getbits = [&](int32_t& v) {
-        v = (int32_t)(x & kMaxBypass);
-        x >>= kBypassPrec;
-        return dec_renorm(x, ptr, end);
-      };
-      int32_t v = 0;
-      ok = getbits(v);
-      int32_t nb = v;
-      while (ok && v == kMaxBypass && nb < 64) {
-        ok = getbits(v);
-        nb += v;
+  int32_t cur[kPf], nxt[kPf];
+#pragma unroll
+  for (int k = 0; k < kPf; ++k) cur[k] = i + k < e ? indexes[i + k] : 0;
+  for (; i < e; i += kPf) {
+#pragma unroll
+    for (int k = 0; k < kPf; ++k) nxt[k] = i + kPf + k < e ? indexes[i + kPf + k] : 0;
+#pragma unroll
+    for (int k = 0; k < kPf; ++k) {
+      const int64_t ik = i + k;
+      if (ik >= e) break;
+      const int32_t ci = cur[k];
+      if (!ok) {
+        symbols[ik] = 0;
+        continue;
       }
-      if (nb > 8) ok = false;
-      uint32_t raw = 0;
-      for (int32_t j = 0; ok && j < nb; ++j) {
+      const uint32_t cum = (uint32_t)(x & mask);
+      const uint32_t* sfc = sft + (size_t)ci * cdf_stride;
+      int32_t sidx = lut[(size_t)ci * kLutN + (cum >> kLutShift)];
+      uint32_t sf = sfc[sidx];
+      while (cum >= (sf & 0xFFFFu) + (sf >> 16)) sf = sfc[++sidx];
+      const uint32_t start = sf & 0xFFFFu, freq = sf >> 16;
+      x = freq * (x >> kPrec) + cum - start;
+      ok = renorm();
+      int32_t value = sidx;
+      if (ok && start + freq == (1u << kPrec)) {  // escape bin (== max_value)
+        auto getbits = [&](int32_t& v) {
+          v = (int32_t)(x & kMaxBypass);
+          x >>= kBypassPrec;
+          return renorm();
+        };
+        int32_t v = 0;
         ok = getbits(v);
-        raw |= (uint32_t)v << (j * kBypassPrec);
+        int32_t nb = v;
+        while (ok && v == kMaxBypass && nb < 64) {
+          ok = getbits(v);
+          nb += v;
+        }
+        if (nb > 8) ok = false;
+        uint32_t raw = 0;
+        for (int32_t j = 0; ok && j < nb; ++j) {
+          ok = getbits(v);
+          raw |= (uint32_t)v << (j * kBypassPrec);
+        }
+        const int32_t max_value = cdf_sizes[ci] - 2;
+        value = (int32_t)(raw >> 1);
+        if (raw & 1) value = -value - 1;
+        else value += max_value;
       }
-      const int32_t max_value = cdf_sizes[ci] - 2;
-      value = (int32_t)(raw >> 1);
-      if (raw & 1) value = -value - 1;
-      else value += max_value;
+      symbols[ik] = value + offsets[ci];
     }
-    symbols[i] = value + offsets[ci];
+#pragma unroll
+    for (int k = 0; k < kPf; ++k) cur[k] = nxt[k];
   }
   status[s] = ok ? 0 : FVC_ECORRUPT;
 }
@@ -379,15 +428,19 @@ int fvc_rans_encode(const int32_t* symbols, const int32_t* indexes, const int64_
   return 0;
 }
 
-size_t fvc_rans_lut_bytes(int ntables) { return (size_t)ntables * (6u << kPrec); }
+size_t fvc_rans_lut_bytes(int ntables, int cdf_stride) {
+  if (ntables <= 0 || cdf_stride <= 1) return 0;
+  return (size_t)ntables * ((size_t)cdf_stride * 4 + (size_t)kLutN * 2);
+}
 
 int fvc_rans_build_lut(const int32_t* cdfs, int cdf_stride, const int32_t* cdf_sizes, int ntables, void* lut,
                        fvc_stream_t s) {
-  if (!cdfs || !cdf_sizes || !lut || ntables <= 0) return FVC_EINVAL;
-  uint32_t* lutsf = (uint32_t*)lut;
-  uint16_t* lut16 = (uint16_t*)(lutsf + ((size_t)ntables << kPrec));
-  hipLaunchKernelGGL(k_build_lut, dim3(grid_for((size_t)ntables << 16)), dim3(kBlk), 0, (hipStream_t)s, cdfs,
-                     cdf_stride, cdf_sizes, ntables, lut16, lutsf);
+  if (!cdfs || !cdf_sizes || !lut || ntables <= 0 || cdf_stride <= 1) return FVC_EINVAL;
+  uint32_t* sf = (uint32_t*)lut;
+  uint16_t* lut16 = (uint16_t*)(sf + (size_t)ntables * cdf_stride);
+  const size_t n = (size_t)ntables * (kLutN + cdf_stride);
+  hipLaunchKernelGGL(k_build_lut, dim3(grid_for(n)), dim3(kBlk), 0, (hipStream_t)s, cdfs, cdf_stride, cdf_sizes,
+                     ntables, lut16, sf);
   FVC_CHECK_LAUNCH();
   return 0;
 }
@@ -404,16 +457,16 @@ int fvc_rans_pack(const uint32_t* words, const int64_t* word_off, const int32_t*
 }
 
 int fvc_rans_decode(const uint32_t* packed, const int64_t* pack_off, const int32_t* indexes, const int64_t* sym_off,
-                    int nstreams, int ntables, const int32_t* cdf_sizes, const int32_t* offsets, const void* lut,
-                    int32_t* symbols, int32_t* status, fvc_stream_t s) {
+                    int nstreams, int ntables, int cdf_stride, const int32_t* cdf_sizes, const int32_t* offsets,
+                    const void* lut, int32_t* symbols, int32_t* status, fvc_stream_t s) {
   if (!packed || !pack_off || !indexes || !sym_off || !cdf_sizes || !offsets || !lut || !symbols || !status ||
-      nstreams <= 0 || ntables <= 0)
+      nstreams <= 0 || ntables <= 0 || cdf_stride <= 1)
     return FVC_EINVAL;
-  const uint32_t* lutsf = (const uint32_t*)lut;
-  const uint16_t* lut16 = (const uint16_t*)(lutsf + ((size_t)ntables << kPrec));
+  const uint32_t* sf = (const uint32_t*)lut;
+  const uint16_t* lut16 = (const uint16_t*)(sf + (size_t)ntables * cdf_stride);
   const int blk = 64;
   hipLaunchKernelGGL(k_rans_decode, dim3((nstreams + blk - 1) / blk), dim3(blk), 0, (hipStream_t)s, packed, pack_off,
-                     indexes, sym_off, nstreams, cdf_sizes, offsets, lut16, lutsf, symbols, status);
+                     indexes, sym_off, nstreams, cdf_stride, cdf_sizes, offsets, lut16, sf, symbols, status);
   FVC_CHECK_LAUNCH();
   return 0;
 }

@@ -548,16 +548,15 @@ static int run_x3(const float* x, const void* wpack, float osc, const float* bia
   if (lds > 160 * 1024) return FVC_EINVAL;
   const int tiles_x = fvc_cdiv(a.Wq, 32);
   const int tiles_y = fvc_cdiv(a.Hq, c.th);
-  // N-tiles per block: as many as divide ntp (max 2, or 4 with FVC_X3_WN=4) while the grid
-  // still has >= 1024 blocks to fill 256 CUs
+  // N-tiles per block: 2 (each staged input element feeds 64 output channels) unless the layer
+  // has too few spatial tiles x N-groups to give every CU of the persistent grid some work
   int wn = c.ntp >= 2 ? 2 : 1;
   const int want_wn = env_int("FVC_X3_WN", 0);
-  if (want_wn == 1 || want_wn == 2 || want_wn == 4) wn = want_wn;
+  if (want_wn == 1 || want_wn == 2) wn = want_wn;
   while (wn > 1 && c.ntp % wn) wn >>= 1;
   const long long base = (long long)tiles_x * tiles_y * batch * c.nclass;
   if (!want_wn)
-    while (wn > 1 && base * (c.ntp / wn) < 1024) wn >>= 1;
-  if (wn > 2) wn = 2;
+    while (wn > 1 && base * (c.ntp / wn) < 2LL * x3_num_cus()) wn >>= 1;
   // persistent grid: ~one 8-wave block per CU (FVC_X3_BPC blocks per CU), each walking a
   // contiguous run of spatial tiles
   const int ncu = x3_num_cus();

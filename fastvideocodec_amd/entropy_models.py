@@ -180,7 +180,8 @@ class RangeCoder:
         self._offs = {}
         nt = self.cdf.shape[0]
         self.ntables = nt
-        self.lut = torch.empty((_lib.load().fvc_rans_lut_bytes(nt) + 3) // 4, dtype=torch.int32, device=self.device)
+        nb = _lib.load().fvc_rans_lut_bytes(nt, self.cdf.shape[1])
+        self.lut = torch.empty((nb + 3) // 4, dtype=torch.int32, device=self.device)
         _lib.call("fvc_rans_build_lut", self.cdf.data_ptr(), self.cdf.shape[1], self.cdf_length.data_ptr(), nt,
                   self.lut.data_ptr(), K.stream_handle(self.device))
 
@@ -227,7 +228,8 @@ class RangeCoder:
         out = torch.empty((S, n), dtype=torch.int32, device=self.device)
         status = torch.empty(S, dtype=torch.int32, device=self.device)
         _lib.call("fvc_rans_decode", enc.packed.data_ptr(), enc.pack_off.data_ptr(), indexes.data_ptr(),
-                  sym_off.data_ptr(), S, self.ntables, self.cdf_length.data_ptr(), self.offset.data_ptr(),
+                  sym_off.data_ptr(), S, self.ntables, self.cdf.shape[1], self.cdf_length.data_ptr(),
+                  self.offset.data_ptr(),
                   self.lut.data_ptr(), out.data_ptr(), status.data_ptr(), K.stream_handle())
         if check and int(status.abs().max()) != 0:
             raise _lib.FvcError("corrupt rANS stream")

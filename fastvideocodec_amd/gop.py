@@ -2,16 +2,19 @@
 models.py:368-383): the I-frame passes through (BPG out of scope), every P-frame is encoded and
 then decoded from its bitstream.
 
-Three HIP streams form a pipeline:
+Four kinds of HIP streams form a pipeline:
   * encoder stream (the caller's current stream): the encoder forward of frame t, using the
     encoder's own reconstruction of frame t-1 as reference (exactly what the reference loop
     does: x_prev = model(...)[0]);
   * coder stream: symbols -> rANS encode of frame t (waits only on frame t's latents);
-  * decoder stream: rANS decode + synthesis of frame t against the decoder's own previous
-    reconstruction (waits only on frame t's bitstream).
+  * entropy-decode streams (two, round-robin over frames): rANS decode of frame t's z ->
+    hyperprior -> feature, and mv (waits only on frame t's bitstream; no reference frame needed,
+    so consecutive frames decode concurrently);
+  * reconstruction stream: mvDecoder + motion compensation + resDecoder of frame t against the
+    decoder's own previous reconstruction (waits on frame t's latents).
 Encoder and decoder reconstructions are bit-identical (same kernels, same operand order;
-checked by tests and by bench.py), so the decoder never gates the encoder, and the three
-pipelines overlap on the GPU.
+checked by tests and by bench.py), so the decoder never gates the encoder, and the pipelines
+overlap on the GPU (the rANS chains are latency-bound on few CUs, beside compute-bound convs).
 
 G GOPs are batched along dim 0 (frame t of every GOP in one forward).
 """
@@ -27,7 +30,7 @@ _STREAMS = {}
 def _side_streams(device):
     key = str(device)
     if key not in _STREAMS:
-        _STREAMS[key] = (torch.cuda.Stream(device=device), torch.cuda.Stream(device=device))
+        _STREAMS[key] = tuple(torch.cuda.Stream(device=device) for _ in range(4))
     return _STREAMS[key]
 
 
@@ -36,7 +39,10 @@ def encode_decode_gop(model, frames: torch.Tensor, check=False, overlap=True):
     list, encoder recons); every returned tensor is ready on the caller's stream."""
     G, T = frames.shape[:2]
     main = torch.cuda.current_stream(frames.device)
-    s_code, s_dec = _side_streams(frames.device) if overlap else (main, main)
+    if overlap:
+        s_code, s_ed0, s_ed1, s_rec = _side_streams(frames.device)
+    else:
+        s_code = s_ed0 = s_ed1 = s_rec = main
     x_enc = frames[:, 0].contiguous()
     x_dec = x_enc
     bitstreams, decoded, sses, enc_recons, keep = [], [], [], [], [x_enc]
@@ -51,15 +57,19 @@ def encode_decode_gop(model, frames: torch.Tensor, check=False, overlap=True):
             s_code.wait_stream(main)
             with torch.cuda.stream(s_code):
                 bs = model.compress_tensors(lat)
-            s_dec.wait_stream(s_code)
-            with torch.cuda.stream(s_dec):
-                rec_dec = model.decompress(bs, x_dec, check=check)
-            keep.append((lat, cur))  # cross-stream tensors stay alive until the pipeline drains
+            s_ed = s_ed0 if t % 2 else s_ed1
+            s_ed.wait_stream(s_code)
+            with torch.cuda.stream(s_ed):
+                dlat = model.decode_latents(bs, check=check)
+            s_rec.wait_stream(s_ed)
+            with torch.cuda.stream(s_rec):
+                rec_dec = model.reconstruct(dlat, x_dec)
+            keep.append((lat, cur, dlat))  # cross-stream tensors stay alive until the pipeline drains
             bitstreams.append(bs)
             decoded.append(rec_dec)
             enc_recons.append(clipped)
             sses.append(sse)
             x_enc, x_dec = clipped, rec_dec
-    main.wait_stream(s_code)
-    main.wait_stream(s_dec)
+    for st in {s_code, s_ed0, s_ed1, s_rec}:
+        main.wait_stream(st)
     return bitstreams, decoded, sses, enc_recons

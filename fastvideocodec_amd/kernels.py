@@ -211,7 +211,7 @@ class PackedConv:
             timer.records.append((ev0, ev1, profiling.conv_flops(self.cin, self.cout, self.ksize, self.stride,
                                                                  self.transposed, B, H, W),
                                   f"{'deconv' if self.transposed else 'conv'}{self.ksize}s{self.stride} "
-                                  f"{self.cin}->{self.cout} @{H}x{W}{' x3' if self.x3 else ''}"))
+                                  f"{self.cin}->{self.cout} @{H}x{W}{' x3' if self.x3 else ''}", self.x3))
         return y
 
 

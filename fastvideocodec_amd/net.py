@@ -455,16 +455,16 @@ class VideoCompressor(nn.Module):
             return bs, clipped, sse
         return bs, clipped
 
-    def decompress(self, bs: PFrameBitstream, referframe, check=True):
-        """Decode a P-frame from its bitstream and the reference frame (z -> sigma -> feature;
-        mv -> motion compensation; residual synthesis)."""
+    def decode_latents(self, bs: PFrameBitstream, check=True):
+        """Entropy-decode a P-frame bitstream into its three quantised latents (NHWC device
+        tensors): z -> respriorDecoder -> sigma -> scale indexes -> feature; mv. Needs no
+        reference frame, so it can run ahead of the reconstruction chain."""
         self.update()
         c = self._coders
         B = bs.batch
         (H16, W16), (H64, W64) = bs.hw16, bs.hw64
-        dev = referframe.device
+        dev = bs.mv.packed.device
         with torch.no_grad():
-            ref4 = K.nchw_to_nhwc(referframe.float().contiguous(), 4)
             idx_z = K.channel_indexes(B, H64 * W64, OUT_CHANNEL_N, dev)
             sym_z = c["z"].decode(bs.z, idx_z.view(-1, H64 * W64), check).view(B, OUT_CHANNEL_N, H64 * W64)
             z = K.symbols_to_latent(sym_z, H64, W64, OUT_CHANNEL_N)
@@ -475,8 +475,19 @@ class VideoCompressor(nn.Module):
             idx_mv = K.channel_indexes(B, H16 * W16, OUT_CHANNEL_MV, dev)
             sym_mv = c["mv"].decode(bs.mv, idx_mv.view(-1, H16 * W16), check).view(B, OUT_CHANNEL_MV, H16 * W16)
             mvq = K.symbols_to_latent(sym_mv, H16, W16, OUT_CHANNEL_MV)
-            mv_up = self.mvDecoder.run(mvq)
-            prediction, warpframe = self.motioncompensation(ref4, mv_up)
-            recon = self.resDecoder.run(feature, prediction)
-            clipped = K.nhwc_to_nchw(recon, 3, clamp01=True)
-        return clipped
+        return {"mv": mvq, "feature": feature, "z": z}
+
+    def reconstruct(self, lat, referframe):
+        """Decoder synthesis from decoded latents: mvDecoder -> motion compensation ->
+        resDecoder (+ prediction) -> clamp. Returns the NCHW reconstruction."""
+        with torch.no_grad():
+            ref4 = K.nchw_to_nhwc(referframe.float().contiguous(), 4)
+            mv_up = self.mvDecoder.run(lat["mv"])
+            prediction, _ = self.motioncompensation(ref4, mv_up)
+            recon = self.resDecoder.run(lat["feature"], prediction)
+            return K.nhwc_to_nchw(recon, 3, clamp01=True)
+
+    def decompress(self, bs: PFrameBitstream, referframe, check=True):
+        """Decode a P-frame from its bitstream and the reference frame (z -> sigma -> feature;
+        mv -> motion compensation; residual synthesis)."""
+        return self.reconstruct(self.decode_latents(bs, check), referframe)

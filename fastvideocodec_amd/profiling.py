@@ -33,12 +33,14 @@ class KernelTimer:
         global _ACTIVE
         _ACTIVE = None
 
-    def collect(self):
-        """Synchronise and return (total_ms, total_flops, n_launches)."""
+    def collect(self, x3=None):
+        """Synchronise and return (total_ms, total_flops, n_launches); x3=True/False restricts to
+        the split-precision / the fp32+VALU conv launches."""
         torch.cuda.synchronize()
-        ms = sum(r[0].elapsed_time(r[1]) for r in self.records)
-        fl = sum(r[2] for r in self.records)
-        return ms, fl, len(self.records)
+        rs = [r for r in self.records if x3 is None or (len(r) > 4 and r[4]) == x3]
+        ms = sum(r[0].elapsed_time(r[1]) for r in rs)
+        fl = sum(r[2] for r in rs)
+        return ms, fl, len(rs)
 
     def breakdown(self):
         """Per-geometry aggregate: {key: [launches, ms, flops]} (keys recorded by the caller)."""

@@ -175,18 +175,18 @@ int fvc_rans_encode(const int32_t* symbols, const int32_t* indexes, const int64_
  * of region s; pack_off is [nstreams+1] (exclusive scan of nwords, computed on device). */
 int fvc_rans_pack(const uint32_t* words, const int64_t* word_off, const int32_t* nwords,
                   int nstreams, int64_t* pack_off, uint32_t* out, fvc_stream_t stream);
-/* Decode lookup tables, built once per table set (fvc_rans_lut_bytes(ntables) bytes):
- * for every table t and cum in [0, 2^16): the symbol index and its (start | freq << 16), so a
- * decoded symbol costs one dependent memory access on the state chain. */
-size_t fvc_rans_lut_bytes(int ntables);
+/* Decode tables, built once per table set (fvc_rans_lut_bytes(ntables, cdf_stride) bytes): per
+ * table a 4096-bucket cum -> first-candidate-symbol map and a start|freq<<16 word per symbol
+ * (L2-resident; a decoded symbol costs two dependent cache hits). */
+size_t fvc_rans_lut_bytes(int ntables, int cdf_stride);
 int fvc_rans_build_lut(const int32_t* cdfs, int cdf_stride, const int32_t* cdf_sizes, int ntables,
                        void* lut, fvc_stream_t stream);
 /* Decode: stream s reads packed words starting at pack_off[s]; status[s] = 0 or FVC_ECORRUPT.
  * Output identical to compressai RansDecoder.decode_with_indexes per stream. */
 int fvc_rans_decode(const uint32_t* packed, const int64_t* pack_off, const int32_t* indexes,
-                    const int64_t* sym_off, int nstreams, int ntables, const int32_t* cdf_sizes,
-                    const int32_t* offsets, const void* lut, int32_t* symbols, int32_t* status,
-                    fvc_stream_t stream);
+                    const int64_t* sym_off, int nstreams, int ntables, int cdf_stride,
+                    const int32_t* cdf_sizes, const int32_t* offsets, const void* lut,
+                    int32_t* symbols, int32_t* status, fvc_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -6,7 +6,7 @@ usage: python scripts/rocprof_summary.py <stats_csv> <n_pframes_total> [fetch_cs
 import csv
 import sys
 
-CONV_PREFIXES = ("conv_mfma_f32_kernel", "conv_mfma_pipe_kernel", "deconv2_mfma_f32_kernel",
+CONV_PREFIXES = ("conv_x3_kernel", "conv_mfma_f32_kernel", "conv_mfma_pipe_kernel", "deconv2_mfma_f32_kernel",
                  "conv_smalln_f32_kernel")
 
 
