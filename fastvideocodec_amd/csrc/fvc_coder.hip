@@ -271,19 +271,25 @@ __global__ void k_build_lut(const int32_t* __restrict__ cdfs, int cdf_stride, co
   }
 }
 
-// One lane per stream. The next bitstream word and the next kPf table indexes are held in
-// registers ahead of need, so the only memory accesses on the state chain are the two table hits.
-__global__ void k_rans_decode(const uint32_t* __restrict__ packed, const int64_t* __restrict__ pack_off,
-                              const int32_t* __restrict__ indexes, const int64_t* __restrict__ sym_off, int nstreams,
-                              int cdf_stride, const int32_t* __restrict__ cdf_sizes,
-                              const int32_t* __restrict__ offsets, const uint16_t* __restrict__ lut,
-                              const uint32_t* __restrict__ sft, int32_t* __restrict__ symbols,
-                              int32_t* __restrict__ status) {
-  const int s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= nstreams) return;
-  const uint32_t* ptr = packed + pack_off[s];
-  const uint32_t* end = packed + pack_off[s + 1];
-  bool ok = end - ptr >= 2;
+// One lane per stream (64-lane blocks). The next bitstream word and the next kPf table indexes
+// are held in registers ahead of need, so the only memory accesses on the state chain are the
+// two table hits. Decoded symbols go to an LDS ring (kRing per lane) and are written to global
+// memory in bursts: a global store outstanding in vmcnt would make every later load wait for it
+// (the compiler cannot order a load behind a store), i.e. one store latency per symbol.
+constexpr int kRing = 64;
+
+__global__ __launch_bounds__(64) void k_rans_decode(
+    const uint32_t* __restrict__ packed, const int64_t* __restrict__ pack_off, const int32_t* __restrict__ indexes,
+    const int64_t* __restrict__ sym_off, int nstreams, int cdf_stride, const int32_t* __restrict__ cdf_sizes,
+    const int32_t* __restrict__ offsets, const uint16_t* __restrict__ lut, const uint32_t* __restrict__ sft,
+    int32_t* __restrict__ symbols, int32_t* __restrict__ status) {
+  __shared__ int32_t ring[kRing * 64];
+  const int lane = threadIdx.x;
+  const int s = blockIdx.x * 64 + lane;
+  const bool live = s < nstreams;
+  const uint32_t* ptr = packed + (live ? pack_off[s] : 0);
+  const uint32_t* end = packed + (live ? pack_off[s + 1] : 0);
+  bool ok = live && end - ptr >= 2;
   uint64_t x = 0;
   if (ok) {
     x = (uint64_t)ptr[0] | ((uint64_t)ptr[1] << 32);
@@ -300,62 +306,78 @@ __global__ void k_rans_decode(const uint32_t* __restrict__ packed, const int64_t
     return true;
   };
   const uint64_t mask = (1ull << kPrec) - 1;
-  const int64_t e = sym_off[s + 1];
-  int64_t i = sym_off[s];
-  int32_t cur[kPf], nxt[kPf];
+  const int64_t b = live ? sym_off[s] : 0;
+  const int64_t e = live ? sym_off[s + 1] : 0;
+  // all lanes walk the same number of steps (the wave's longest stream); shorter ones idle
+  int64_t len = e - b, maxlen = len;
+  for (int o = 32; o > 0; o >>= 1) {
+    const int64_t v = __shfl_xor(maxlen, o, 64);
+    maxlen = v > maxlen ? v : maxlen;
+  }
+  int32_t cur[kPf], nxt[kPf], off[kPf];
 #pragma unroll
-  for (int k = 0; k < kPf; ++k) cur[k] = i + k < e ? indexes[i + k] : 0;
-  for (; i < e; i += kPf) {
+  for (int k = 0; k < kPf; ++k) cur[k] = k < len ? indexes[b + k] : 0;
 #pragma unroll
-    for (int k = 0; k < kPf; ++k) nxt[k] = i + kPf + k < e ? indexes[i + kPf + k] : 0;
+  for (int k = 0; k < kPf; ++k) off[k] = offsets[cur[k]];
+  auto flush = [&](int64_t base, int n) {  // symbols [base, base+n) of this lane from the ring
+    for (int j = 0; j < n; ++j)
+      if (base + j < len) symbols[b + base + j] = ring[j * 64 + lane];
+  };
+  for (int64_t i = 0; i < maxlen; i += kPf) {
+#pragma unroll
+    for (int k = 0; k < kPf; ++k) nxt[k] = i + kPf + k < len ? indexes[b + i + kPf + k] : 0;
 #pragma unroll
     for (int k = 0; k < kPf; ++k) {
       const int64_t ik = i + k;
-      if (ik >= e) break;
       const int32_t ci = cur[k];
-      if (!ok) {
-        symbols[ik] = 0;
-        continue;
-      }
-      const uint32_t cum = (uint32_t)(x & mask);
-      const uint32_t* sfc = sft + (size_t)ci * cdf_stride;
-      int32_t sidx = lut[(size_t)ci * kLutN + (cum >> kLutShift)];
-      uint32_t sf = sfc[sidx];
-      while (cum >= (sf & 0xFFFFu) + (sf >> 16)) sf = sfc[++sidx];
-      const uint32_t start = sf & 0xFFFFu, freq = sf >> 16;
-      x = freq * (x >> kPrec) + cum - start;
-      ok = renorm();
-      int32_t value = sidx;
-      if (ok && start + freq == (1u << kPrec)) {  // escape bin (== max_value)
-        auto getbits = [&](int32_t& v) {
-          v = (int32_t)(x & kMaxBypass);
-          x >>= kBypassPrec;
-          return renorm();
-        };
-        int32_t v = 0;
-        ok = getbits(v);
-        int32_t nb = v;
-        while (ok && v == kMaxBypass && nb < 64) {
+      int32_t value = 0;
+      if (ik < len && ok) {
+        const uint32_t cum = (uint32_t)(x & mask);
+        const uint32_t* sfc = sft + (size_t)ci * cdf_stride;
+        int32_t sidx = lut[(size_t)ci * kLutN + (cum >> kLutShift)];
+        uint32_t sf = sfc[sidx];
+        while (cum >= (sf & 0xFFFFu) + (sf >> 16)) sf = sfc[++sidx];
+        const uint32_t start = sf & 0xFFFFu, freq = sf >> 16;
+        x = freq * (x >> kPrec) + cum - start;
+        ok = renorm();
+        value = sidx;
+        if (ok && start + freq == (1u << kPrec)) {  // escape bin (== max_value)
+          auto getbits = [&](int32_t& v) {
+            v = (int32_t)(x & kMaxBypass);
+            x >>= kBypassPrec;
+            return renorm();
+          };
+          int32_t v = 0;
           ok = getbits(v);
-          nb += v;
+          int32_t nb = v;
+          while (ok && v == kMaxBypass && nb < 64) {
+            ok = getbits(v);
+            nb += v;
+          }
+          if (nb > 8) ok = false;
+          uint32_t raw = 0;
+          for (int32_t j = 0; ok && j < nb; ++j) {
+            ok = getbits(v);
+            raw |= (uint32_t)v << (j * kBypassPrec);
+          }
+          const int32_t max_value = cdf_sizes[ci] - 2;
+          value = (int32_t)(raw >> 1);
+          if (raw & 1) value = -value - 1;
+          else value += max_value;
         }
-        if (nb > 8) ok = false;
-        uint32_t raw = 0;
-        for (int32_t j = 0; ok && j < nb; ++j) {
-          ok = getbits(v);
-          raw |= (uint32_t)v << (j * kBypassPrec);
-        }
-        const int32_t max_value = cdf_sizes[ci] - 2;
-        value = (int32_t)(raw >> 1);
-        if (raw & 1) value = -value - 1;
-        else value += max_value;
+        value += off[k];
       }
-      symbols[ik] = value + offsets[ci];
+      ring[(int)(ik % kRing) * 64 + lane] = value;
     }
+    if ((i + kPf) % kRing == 0) flush(i + kPf - kRing, kRing);
 #pragma unroll
     for (int k = 0; k < kPf; ++k) cur[k] = nxt[k];
+#pragma unroll
+    for (int k = 0; k < kPf; ++k) off[k] = offsets[cur[k]];
   }
-  status[s] = ok ? 0 : FVC_ECORRUPT;
+  const int64_t done = (maxlen + kPf - 1) / kPf * kPf;  // steps written to the ring
+  if (done % kRing) flush(done - done % kRing, (int)(done % kRing));
+  if (live) status[s] = ok ? 0 : FVC_ECORRUPT;
 }
 
 static int grid_for(size_t n) {
