@@ -52,6 +52,7 @@ struct ConvArgs {
   long long wcls[4];       // float offset of each class in the weight pack
   short tdy[4][kMaxTaps];
   short tdx[4][kMaxTaps];
+  int gy0[4], gny[4], gx0[4], gnx[4];  // per class: tap offsets form [gy0, gy0+gny) x [gx0, gx0+gnx)
 };
 
 template <int CC>
@@ -510,27 +511,32 @@ __global__ __launch_bounds__(kThreads) void deconv2_mfma_f32_kernel(const ConvAr
   }
 }
 
-// Small-N variant (cout <= 4: SpyNet conv5, Warp_net conv6, mvDecoder deconv8, resDecoder
-// deconv4). Padding N to an MFMA tile of 32 would waste 8-16x of the matrix work, so this path is
-// VALU: each lane owns a column of PY output pixels x COUTP channels; the chunk's weights are
-// staged in LDS once and read as wave-uniform broadcasts, reused across the PY pixels; the input
-// comes from the same conflict-free LDS halo tile layout as the MFMA kernel.
-constexpr int kSmallPY = 4;
-
-template <int CC, int COUTP>
+// Small-N variant (cout <= 4: SpyNet conv5, Warp_net conv6, mvDecoder conv8, resDecoder deconv4;
+// stride-1 input steps, i.e. stride-1 convs and the parity classes of transposed convs). Padding
+// N to an MFMA tile would waste 8-16x of the matrix work, so this path is VALU. Each lane owns a
+// column of PY output rows; a class's taps form a contiguous ny x nx grid of input offsets, so
+// for every tap column dx the lane loads the PY + KMAX - 1 input pixels of its column once from
+// the LDS halo tile and reuses each for all tap rows and output rows. The chunk's weights sit in
+// LDS as [KMAX][nx][CC][COUT] (rows past ny zero-filled, so the unrolled tap loop has no branches)
+// and are read as wave-uniform broadcasts. The next chunk's halo is prefetched into registers
+// while the current one is multiplied.
+// Block tile = 8 lane-rows x PY rows x 32 columns. Wide inputs use CC = 32 channels per chunk
+// (a pixel's chunk is one full 128-B line, so no line is fetched once per 8-channel slice) with
+// PY = 2 to keep the halo tile in LDS; narrow inputs use PY = 4.
+template <int CC, int COUT, int KMAX, int PY>
 __global__ __launch_bounds__(kThreads) void conv_smalln_f32_kernel(const ConvArgs a) {
   using G = ChunkGeom<CC>;
   constexpr int CC4 = G::CC4;
   constexpr int CS = G::CS;
   constexpr int TW = 32;
-  constexpr int PY = kSmallPY;
   constexpr int TH = (kThreads / TW) * PY;
+  constexpr int NV = PY + KMAX - 1;
+  constexpr int NPF = ((TH + KMAX - 1) * (TW + KMAX - 1) * CC4 + kThreads - 1) / kThreads;
 
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  int* tap_off = reinterpret_cast<int*>(smem);
-  float* wl = smem + 64;                                   // [ntaps][CC][COUTP]
-  const int ntaps = a.ntaps[blockIdx.z % a.nclass];
-  float* tile = wl + ((ntaps * CC * COUTP + 3) & ~3);
+  const int nx = a.gnx[blockIdx.z % a.nclass];
+  float* const wl = smem;                                          // [KMAX][nx][CC][COUT]
+  float* const tile = smem + ((KMAX * nx * CC * COUT + 3) & ~3);   // + KMAX-1 spare rows
 
   const int tid = threadIdx.x;
   const int tx = tid & (TW - 1);
@@ -540,66 +546,92 @@ __global__ __launch_bounds__(kThreads) void conv_smalln_f32_kernel(const ConvArg
   const int tiles_x = (a.Wq + TW - 1) / TW;
   const int qy0 = (blockIdx.x / tiles_x) * TH;
   const int qx0 = (blockIdx.x % tiles_x) * TW;
+  const int ny = a.gny[cls];
+  const int coutp = a.coutp;
 
-  if (tid < ntaps)
-    tap_off[tid] = ((a.tdy[cls][tid] - a.dymin) * a.ic + (a.tdx[cls][tid] - a.dxmin)) * CS;
-
-  float acc[PY][COUTP];
+  float acc[PY][COUT];
 #pragma unroll
   for (int k = 0; k < PY; ++k)
 #pragma unroll
-    for (int j = 0; j < COUTP; ++j) acc[k][j] = 0.f;
+    for (int j = 0; j < COUT; ++j) acc[k][j] = 0.f;
 
-  const int iy0 = qy0 * a.sin + a.dymin;
-  const int ix0 = qx0 * a.sin + a.dxmin;
+  const int iy0 = qy0 + a.dymin;
+  const int ix0 = qx0 + a.dxmin;
   const int tile_elems = a.ir * a.ic * CC4;
   const float* xb = a.x + (size_t)b * a.H * a.W * a.cinp;
-  const int pix_base = ((ty * PY * a.sin) * a.ic + tx * a.sin) * CS;
-  const int row_step = a.sin * a.ic * CS;
+  // LDS base of this lane's column at the class grid origin
+  const int col0 = ((ty * PY + a.gy0[cls] - a.dymin) * a.ic + tx + a.gx0[cls] - a.dxmin) * CS;
+  const int row_step = a.ic * CS;
   const float* __restrict__ wcls = a.w + a.wcls[cls];
-  const int wl_elems = ntaps * CC * COUTP;
+  const int wl_n = KMAX * nx * CC * COUT;
 
-  for (int ch = 0; ch < a.nchunks; ++ch) {
-    for (int e = tid; e < tile_elems; e += kThreads) {
-      const int c4 = e % CC4;
-      const int p = e / CC4;
-      const int r = p / a.ic;
-      const int c = p - r * a.ic;
-      const int iy = iy0 + r;
-      const int ix = ix0 + c;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (iy >= 0 && iy < a.H && ix >= 0 && ix < a.W) {
-        v = *reinterpret_cast<const float4*>(xb + ((size_t)iy * a.W + ix) * a.cinp + ch * CC + c4 * 4);
-        v = fvc_in_op_sel4(v, a.in_op);
+  float4 pf[NPF];
+  auto fetch = [&](int ch) {
+#pragma unroll
+    for (int k = 0; k < NPF; ++k) {
+      const int e = tid + k * kThreads;
+      pf[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (e < tile_elems) {
+        const int c4 = e % CC4;
+        const int p = e / CC4;
+        const int r = p / a.ic;
+        const int c = p - r * a.ic;
+        const int iy = iy0 + r;
+        const int ix = ix0 + c;
+        if (iy >= 0 && iy < a.H && ix >= 0 && ix < a.W)
+          pf[k] = *reinterpret_cast<const float4*>(xb + ((size_t)iy * a.W + ix) * a.cinp + ch * CC + c4 * 4);
       }
-      *reinterpret_cast<float4*>(tile + p * CS + c4 * 4) = v;
     }
-    const float* wch = wcls + (size_t)ch * wl_elems;
-    for (int e = tid; e < wl_elems; e += kThreads) wl[e] = wch[e];
+  };
+  auto put = [&](int ch) {
+#pragma unroll
+    for (int k = 0; k < NPF; ++k) {
+      const int e = tid + k * kThreads;
+      if (e < tile_elems) {
+        const int c4 = e % CC4;
+        const int p = e / CC4;
+        *reinterpret_cast<float4*>(tile + p * CS + c4 * 4) = fvc_in_op_sel4(pf[k], a.in_op);
+      }
+    }
+    // weights of this chunk: pack [dy][dx][cin][coutp] -> LDS [KMAX][nx][CC][COUT], zero rows past ny
+    const float* wch = wcls + (size_t)ch * ny * nx * CC * coutp;
+    for (int e = tid; e < wl_n; e += kThreads) {
+      const int j = e % COUT;
+      const int r = e / COUT;  // (dy * nx + dx) * CC + c
+      wl[e] = r < ny * nx * CC ? wch[(size_t)r * coutp + j] : 0.f;
+    }
+  };
+
+  // spare rows below the halo tile: read (times zero weights) by the branch-free tap loop, so
+  // they must hold finite values
+  for (int e = tile_elems * 4 + tid; e < (a.ir + KMAX - 1) * a.ic * CS; e += kThreads) tile[e] = 0.f;
+  fetch(0);
+  for (int ch = 0; ch < a.nchunks; ++ch) {
+    put(ch);
     __syncthreads();
-    for (int t = 0; t < ntaps; ++t) {
-      const int toff = tap_off[t];
-      const float* wt = wl + t * CC * COUTP;
+    if (ch + 1 < a.nchunks) fetch(ch + 1);
+    for (int dxi = 0; dxi < nx; ++dxi) {
+      const float* colp = tile + col0 + dxi * CS;
 #pragma unroll
       for (int c4 = 0; c4 < CC4; ++c4) {
-        float4 v[PY];
+        float4 v[NV];
 #pragma unroll
-        for (int k = 0; k < PY; ++k)
-          v[k] = *reinterpret_cast<const float4*>(tile + pix_base + k * row_step + toff + c4 * 4);
+        for (int r = 0; r < NV; ++r) v[r] = *reinterpret_cast<const float4*>(colp + r * row_step + c4 * 4);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          float wv[COUTP];
+        for (int dyi = 0; dyi < KMAX; ++dyi) {
+          const float* wt = wl + ((dyi * nx + dxi) * CC + c4 * 4) * COUT;
+          float wv[4 * COUT];
 #pragma unroll
-          for (int j4 = 0; j4 < COUTP / 4; ++j4) {
-            const float4 w4 = *reinterpret_cast<const float4*>(wt + (c4 * 4 + e) * COUTP + j4 * 4);
-            wv[j4 * 4] = w4.x; wv[j4 * 4 + 1] = w4.y; wv[j4 * 4 + 2] = w4.z; wv[j4 * 4 + 3] = w4.w;
-          }
+          for (int u = 0; u < 4 * COUT; ++u) wv[u] = wt[u];
 #pragma unroll
-          for (int k = 0; k < PY; ++k) {
-            const float xv = e == 0 ? v[k].x : (e == 1 ? v[k].y : (e == 2 ? v[k].z : v[k].w));
+          for (int e = 0; e < 4; ++e)
 #pragma unroll
-            for (int j = 0; j < COUTP; ++j) acc[k][j] = __builtin_fmaf(xv, wv[j], acc[k][j]);
-          }
+            for (int k = 0; k < PY; ++k) {
+              const float4 xv = v[k + dyi];
+              const float xs = e == 0 ? xv.x : (e == 1 ? xv.y : (e == 2 ? xv.z : xv.w));
+#pragma unroll
+              for (int j = 0; j < COUT; ++j) acc[k][j] = __builtin_fmaf(xs, wv[e * COUT + j], acc[k][j]);
+            }
         }
       }
     }
@@ -614,33 +646,32 @@ __global__ __launch_bounds__(kThreads) void conv_smalln_f32_kernel(const ConvArg
     const int qy = qy0 + ty * PY + k;
     if (qy >= a.Hq) continue;
     const int oy = qy * a.sout + a.oy0[cls];
-    const size_t o = (((size_t)b * a.Ho + oy) * a.Wo + ox) * a.coutp;
+    const size_t o = (((size_t)b * a.Ho + oy) * a.Wo + ox) * coutp;
+    float r4[4];
 #pragma unroll
-    for (int j4 = 0; j4 < COUTP / 4; ++j4) {
-      float r4[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int j = j4 * 4 + u;
-        float v = acc[k][j] + (j < a.cout ? a.bias[j] : 0.f);
+    for (int j = 0; j < 4; ++j) {
+      float v = j < COUT ? acc[k][j < COUT ? j : 0] + a.bias[j] : 0.f;
+      if (j < COUT) {
         if (a.act == FVC_ACT_RELU) v = v > 0.f ? v : 0.f;
         else if (a.act == FVC_ACT_LRELU) v = v > 0.f ? v : 0.1f * v;
         if (a.res) v += a.res[o + j];
         if (a.post_op == FVC_POST_EXP) v = expf(v);
-        r4[u] = j < a.cout ? v : 0.f;
       }
-      *reinterpret_cast<float4*>(a.y + o + j4 * 4) = make_float4(r4[0], r4[1], r4[2], r4[3]);
+      r4[j] = v;
     }
+    *reinterpret_cast<float4*>(a.y + o) = make_float4(r4[0], r4[1], r4[2], r4[3]);
   }
 }
 
 // ------------------------------------------------------------------ host-side geometry
 struct Cfg {
-  int cinp, coutp, ntp, cc, wm, wn, nclass, nchunks, smalln, fused, th, pipe, nw, lds_bufs;
+  int cinp, coutp, ntp, cc, wm, wn, nclass, nchunks, smalln, sn_py, fused, th, pipe, nw, lds_bufs;
   int sin, sout;
   int ntaps[4], kbc[4], oy0[4], ox0[4];
   int tky[4][kMaxTaps], tkx[4][kMaxTaps];  // kernel tap (ky,kx)
   int tdy[4][kMaxTaps], tdx[4][kMaxTaps];  // input offsets
   int dymin, dymax, dxmin, dxmax;
+  int gy0[4], gny[4], gx0[4], gnx[4];
   long long wcls[4];
   long long wtotal;
 };
@@ -697,8 +728,21 @@ static bool make_cfg(int cin, int cout, int ks, int stride, int transposed, Cfg&
       c.dxmin = c.tdx[cl][t] < c.dxmin ? c.tdx[cl][t] : c.dxmin;
       c.dxmax = c.tdx[cl][t] > c.dxmax ? c.tdx[cl][t] : c.dxmax;
     }
+  for (int cl = 0; cl < c.nclass; ++cl) {
+    int y0 = 1 << 20, y1 = -(1 << 20), x0 = 1 << 20, x1 = -(1 << 20);
+    for (int t = 0; t < c.ntaps[cl]; ++t) {
+      y0 = c.tdy[cl][t] < y0 ? c.tdy[cl][t] : y0;
+      y1 = c.tdy[cl][t] > y1 ? c.tdy[cl][t] : y1;
+      x0 = c.tdx[cl][t] < x0 ? c.tdx[cl][t] : x0;
+      x1 = c.tdx[cl][t] > x1 ? c.tdx[cl][t] : x1;
+    }
+    c.gy0[cl] = y0; c.gny[cl] = y1 - y0 + 1;
+    c.gx0[cl] = x0; c.gnx[cl] = x1 - x0 + 1;
+    if (c.gny[cl] * c.gnx[cl] != c.ntaps[cl]) return false;  // taps always form a full grid
+  }
   c.wn = c.ntp;
-  c.smalln = c.coutp <= 4 ? 1 : 0;  // cout 2/3: MFMA N-tile padding would waste 8-16x
+  // cout 2/3: MFMA N-tile padding would waste 8-16x -> VALU kernel (stride-1 input steps only)
+  c.smalln = (c.coutp <= 4 && c.sin == 1) ? 1 : 0;
   c.fused = (transposed && stride == 2 && !c.smalln && c.cinp % 8 == 0 && ks <= 5) ? 1 : 0;
   {
     // measured: the per-class launch with WN<=2 beats the 4-class fused block (register-bound
@@ -735,7 +779,8 @@ static bool make_cfg(int cin, int cout, int ks, int stride, int transposed, Cfg&
     if (wn1 && wn1[0] == '1' && !c.smalln) c.wn = 1;
   }
   c.lds_bufs = c.pipe ? 2 : 1;
-  c.th = c.smalln ? (kThreads / 32) * kSmallPY : (c.pipe ? c.nw * c.wm : 4 * c.wm);
+  c.sn_py = (c.smalln && c.cinp % 32 == 0) ? 2 : 4;
+  c.th = c.smalln ? (kThreads / 32) * c.sn_py : (c.pipe ? c.nw * c.wm : 4 * c.wm);
   int cc = 32;
   for (;; cc >>= 1) {
     if (cc == 4) break;
@@ -743,8 +788,17 @@ static bool make_cfg(int cin, int cout, int ks, int stride, int transposed, Cfg&
     const int ir = (c.th - 1) * c.sin + 1 + (c.dymax - c.dymin);
     const int ic = 31 * c.sin + 1 + (c.dxmax - c.dxmin);
     const int cs = ((cc / 4) % 2 == 1) ? cc : cc + 4;
-    const size_t wbytes = c.smalln ? (size_t)((maxt * cc * c.coutp + 3) & ~3) * 4 : 0;
-    const size_t budget = (c.pipe && c.nw == 8) ? 100 * 1024 : 64 * 1024;
+    size_t wbytes = 0;
+    if (c.smalln) {
+      int kmx = 0, nxm = 0;
+      for (int cl = 0; cl < c.nclass; ++cl) {
+        kmx = c.gny[cl] > kmx ? c.gny[cl] : kmx;
+        nxm = c.gnx[cl] > nxm ? c.gnx[cl] : nxm;
+      }
+      const int kt = kmx <= 3 ? 3 : (kmx <= 5 ? 5 : 7);
+      wbytes = (size_t)((kt * nxm * cc * 4 + 3) & ~3) * 4 + (size_t)(kt - 1) * ic * cs * 4;
+    }
+    const size_t budget = (c.pipe && c.nw == 8) ? 100 * 1024 : (c.smalln && c.sn_py == 2 ? 112 * 1024 : 64 * 1024);
     if ((size_t)c.lds_bufs * (((size_t)ir * ic * cs + 3) & ~(size_t)3) * 4 + 256 + wbytes <= budget) break;
   }
   {
@@ -760,7 +814,7 @@ static bool make_cfg(int cin, int cout, int ks, int stride, int transposed, Cfg&
   for (int cl = 0; cl < c.nclass; ++cl) {
     c.kbc[cl] = fvc_rup(c.ntaps[cl] * (cc / 4), 2);
     c.wcls[cl] = off;
-    if (c.smalln)  // [chunk][tap][cin in chunk][coutp]
+    if (c.smalln)  // [chunk][dy][dx][cin in chunk][coutp] (tap grid order)
       off += (long long)c.nchunks * c.ntaps[cl] * cc * c.coutp;
     else           // [chunk][k-block][n-tile][32][4]
       off += (long long)c.nchunks * c.kbc[cl] * c.ntp * 128;
@@ -807,20 +861,38 @@ static int launch_wm(int wm, int wn, const ConvArgs& a, dim3 grid, size_t lds, h
   return launch_wn<CC, 2>(wn, a, grid, lds, s);
 }
 
-template <int CC, int COUTP>
-static int launch_sn_t(const ConvArgs& a, dim3 grid, dim3 blk, size_t lds, hipStream_t s) {
-  hipLaunchKernelGGL((conv_smalln_f32_kernel<CC, COUTP>), grid, blk, lds, s, a);
+template <int CC, int COUT, int KMAX>
+static int launch_sn_t(int py, const ConvArgs& a, dim3 grid, dim3 blk, size_t lds, hipStream_t s) {
+  if (py == 2) {
+    if (lds > 64 * 1024)
+      (void)hipFuncSetAttribute((const void*)conv_smalln_f32_kernel<CC, COUT, KMAX, 2>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL((conv_smalln_f32_kernel<CC, COUT, KMAX, 2>), grid, blk, lds, s, a);
+  } else {
+    if (lds > 64 * 1024)
+      (void)hipFuncSetAttribute((const void*)conv_smalln_f32_kernel<CC, COUT, KMAX, 4>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL((conv_smalln_f32_kernel<CC, COUT, KMAX, 4>), grid, blk, lds, s, a);
+  }
   FVC_CHECK_LAUNCH();
   return 0;
 }
 
+template <int CC, int COUT>
+static int launch_sn_k(int kmax, int py, const ConvArgs& a, dim3 grid, dim3 blk, size_t lds, hipStream_t s) {
+  if (kmax <= 3) return launch_sn_t<CC, COUT, 3>(py, a, grid, blk, lds, s);
+  if (kmax <= 5) return launch_sn_t<CC, COUT, 5>(py, a, grid, blk, lds, s);
+  return launch_sn_t<CC, COUT, 7>(py, a, grid, blk, lds, s);
+}
+
 template <int CC>
-static int launch_sn_n(int coutp, const ConvArgs& a, dim3 grid, dim3 blk, size_t lds, hipStream_t s) {
-  switch (coutp) {
-    case 4: return launch_sn_t<CC, 4>(a, grid, blk, lds, s);
-    case 8: return launch_sn_t<CC, 8>(a, grid, blk, lds, s);
-    case 12: return launch_sn_t<CC, 12>(a, grid, blk, lds, s);
-    case 16: return launch_sn_t<CC, 16>(a, grid, blk, lds, s);
+static int launch_sn_n(int cout, int kmax, int py, const ConvArgs& a, dim3 grid, dim3 blk, size_t lds,
+                       hipStream_t s) {
+  switch (cout) {
+    case 1: return launch_sn_k<CC, 1>(kmax, py, a, grid, blk, lds, s);
+    case 2: return launch_sn_k<CC, 2>(kmax, py, a, grid, blk, lds, s);
+    case 3: return launch_sn_k<CC, 3>(kmax, py, a, grid, blk, lds, s);
+    case 4: return launch_sn_k<CC, 4>(kmax, py, a, grid, blk, lds, s);
   }
   return FVC_EINVAL;
 }
@@ -886,12 +958,13 @@ static int launch_fused(int cc, int wn, const ConvArgs& a, dim3 grid, size_t lds
   return FVC_EINVAL;
 }
 
-static int launch_smalln(int cc, int coutp, const ConvArgs& a, dim3 grid, dim3 blk, size_t lds, hipStream_t s) {
+static int launch_smalln(int cc, int cout, int kmax, int py, const ConvArgs& a, dim3 grid, dim3 blk, size_t lds,
+                         hipStream_t s) {
   switch (cc) {
-    case 4: return launch_sn_n<4>(coutp, a, grid, blk, lds, s);
-    case 8: return launch_sn_n<8>(coutp, a, grid, blk, lds, s);
-    case 16: return launch_sn_n<16>(coutp, a, grid, blk, lds, s);
-    case 32: return launch_sn_n<32>(coutp, a, grid, blk, lds, s);
+    case 4: return launch_sn_n<4>(cout, kmax, py, a, grid, blk, lds, s);
+    case 8: return launch_sn_n<8>(cout, kmax, py, a, grid, blk, lds, s);
+    case 16: return launch_sn_n<16>(cout, kmax, py, a, grid, blk, lds, s);
+    case 32: return launch_sn_n<32>(cout, kmax, py, a, grid, blk, lds, s);
   }
   return FVC_EINVAL;
 }
@@ -926,6 +999,10 @@ static int run_conv(const float* x, const float* wpack, const float* bias, const
     a.oy0[cl] = cl < c.nclass ? c.oy0[cl] : 0;
     a.ox0[cl] = cl < c.nclass ? c.ox0[cl] : 0;
     a.wcls[cl] = cl < c.nclass ? c.wcls[cl] : 0;
+    a.gy0[cl] = cl < c.nclass ? c.gy0[cl] : 0;
+    a.gny[cl] = cl < c.nclass ? c.gny[cl] : 0;
+    a.gx0[cl] = cl < c.nclass ? c.gx0[cl] : 0;
+    a.gnx[cl] = cl < c.nclass ? c.gnx[cl] : 0;
     for (int t = 0; t < kMaxTaps; ++t) {
       const bool v = cl < c.nclass && t < c.ntaps[cl];
       a.tdy[cl][t] = (short)(v ? c.tdy[cl][t] : 0);
@@ -935,7 +1012,15 @@ static int run_conv(const float* x, const float* wpack, const float* bias, const
   const int cs = ((c.cc / 4) % 2 == 1) ? c.cc : c.cc + 4;
   int maxt = 0;
   for (int cl = 0; cl < c.nclass; ++cl) maxt = c.ntaps[cl] > maxt ? c.ntaps[cl] : maxt;
-  const size_t wbytes = c.smalln ? (size_t)((maxt * c.cc * c.coutp + 3) & ~3) * 4 : 0;
+  int kmx = 0, nxm = 0;
+  for (int cl = 0; cl < c.nclass; ++cl) {
+    kmx = c.gny[cl] > kmx ? c.gny[cl] : kmx;
+    nxm = c.gnx[cl] > nxm ? c.gnx[cl] : nxm;
+  }
+  const int kmax_t = kmx <= 3 ? 3 : (kmx <= 5 ? 5 : 7);
+  const size_t wbytes = c.smalln ? ((size_t)((kmax_t * nxm * c.cc * cout + 3) & ~3) * 4 +
+                                    (size_t)(kmax_t - 1) * a.ic * cs * 4)
+                                 : 0;
   const size_t lds = 256 + wbytes + (size_t)c.lds_bufs * (((size_t)a.ir * a.ic * cs + 3) & ~(size_t)3) * 4;
   const int tiles_x = fvc_cdiv(a.Wq, 32);
   const int tiles_y = fvc_cdiv(a.Hq, TH);
@@ -955,7 +1040,9 @@ static int run_conv(const float* x, const float* wpack, const float* bias, const
   }
   if (c.smalln) {
     dim3 grid(tiles_x * tiles_y, 1, batch * c.nclass);
-    return launch_smalln(c.cc, c.coutp, a, grid, dim3(kThreads), lds, s);
+    int kmax = 0;
+    for (int cl = 0; cl < c.nclass; ++cl) kmax = c.gny[cl] > kmax ? c.gny[cl] : kmax;
+    return launch_smalln(c.cc, cout, kmax, c.sn_py, a, grid, dim3(kThreads), lds, s);
   }
   if (c.fused) {
     dim3 grid(tiles_x * tiles_y, c.ntp / c.wn, batch);
@@ -1004,8 +1091,10 @@ int fvc_conv_pack_weight(const float* w, float* wp, int cin, int cout, int ks, i
             const float v = transposed ? w[(((size_t)ci * cout + j) * ks + ky) * ks + kx]
                                        : w[(((size_t)j * cin + ci) * ks + ky) * ks + kx];
             size_t o;
-            if (c.smalln)
-              o = (size_t)c.wcls[cl] + (((size_t)ch * c.ntaps[cl] + t) * c.cc + c4 * 4 + e) * c.coutp + j;
+            if (c.smalln) {
+              const int g = (c.tdy[cl][t] - c.gy0[cl]) * c.gnx[cl] + (c.tdx[cl][t] - c.gx0[cl]);
+              o = (size_t)c.wcls[cl] + (((size_t)ch * c.ntaps[cl] + g) * c.cc + c4 * 4 + e) * c.coutp + j;
+            }
             else
               o = (size_t)c.wcls[cl] + (((size_t)ch * c.kbc[cl] + kb) * c.ntp * 32 + j) * 4 + e;
             wp[o] = v;

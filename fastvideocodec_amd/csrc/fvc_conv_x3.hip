@@ -256,10 +256,10 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(const X3Args a) {
         mfmas(use);
         __builtin_amdgcn_sched_barrier(0);
       };
-      auto half_stage = [&](int q, const Ops& use, Ops& nxt_ops) {
+      auto half_stage = [&](int item, int q, const Ops& use, Ops& nxt_ops) {
         load(q + 1 < nq ? q + 1 : nq - 1, nxt_ops);
         Stage st;
-        fetch(tid + q * NT, s_tile, s_ch, st);
+        fetch(item, s_tile, s_ch, st);
         __builtin_amdgcn_sched_barrier(0);
         mfmas(use);
         __builtin_amdgcn_sched_barrier(0);
@@ -267,20 +267,29 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(const X3Args a) {
       };
       Ops S0, S1;
       load(0, S0);
+      // staging items of the next chunk are spread evenly over the k-step pairs (one per staged
+      // pair) so their VALU work interleaves with MFMA-only steps instead of bunching up at the
+      // chunk start, where every wave would be VALU-bound at once
       const int npair = nq >> 1;
-      const int spair = stage_next ? min((nstage + 1) >> 1, npair) : 0;
-      int q = 0;
-      for (int p = 0; p < spair; ++p, q += 2) {
-        half_stage(q, S0, S1);
-        half_stage(q + 1, S1, S0);
+      const int nst = stage_next ? min(nstage, npair) : 0;
+      const int spread = nst ? max(1, npair / nst) : 1;
+      int q = 0, staged = 0;
+      for (; staged < nst; ++staged) {
+        half_stage(tid + staged * NT, q, S0, S1);
+        half_plain(q + 1, S1, S0);
+        q += 2;
+        for (int r = 1; r < spread; ++r, q += 2) {
+          half_plain(q, S0, S1);
+          half_plain(q + 1, S1, S0);
+        }
       }
-      for (int p = spair; p < npair; ++p, q += 2) {
+      for (; q + 1 < nq; q += 2) {
         half_plain(q, S0, S1);
         half_plain(q + 1, S1, S0);
       }
       if (nq & 1) mfmas(S0);
       if (stage_next) {
-        for (int qs = 2 * spair; qs < nstage; ++qs) {
+        for (int qs = staged; qs < nstage; ++qs) {
           Stage st;
           fetch(tid + qs * NT, s_tile, s_ch, st);
           store(nxt, st);
@@ -315,7 +324,7 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(const X3Args a) {
           const float t = fmaf(cor[m][n][r], a.osc_c, acc[m][n][r] * a.osc) + bj;
           v[r] = fmaxf(t, t * a.act_slope);
         }
-        if (a.res) {
+        if (a.res && j < a.coutp) {  // lanes past coutp (cout <= 4 layers) must not read: OOB
           const float* rr = a.res + row;
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
@@ -365,7 +374,14 @@ static bool x3_cfg(int cin, int cout, int ks, int stride, int transposed, X3Cfg&
     return false;
   c.cinp = fvc_rup(cin, 4);
   c.coutp = fvc_rup(cout, 4);
-  if (c.cinp % 8 || c.coutp <= 4) return false;
+  if (c.cinp % 8) return false;
+  // cout <= 4 (N padded to one 32-wide tile): measured faster than the VALU small-N kernel for the
+  // 3x3 / 5x5 layers (Warp_net conv6, mvDecoder conv8, resDecoder deconv4), slower for SpyNet's
+  // 7x7 16->2 (scripts/conv_micro.py); FVC_X3_SMALLN=0/1 forces either way
+  if (c.coutp <= 4) {
+    const int sn = env_int("FVC_X3_SMALLN", -1);
+    if (sn == 0 || (sn < 0 && ks > 5)) return false;
+  }
   c.ntp = fvc_cdiv(c.coutp, 32);
   if (c.ntp > 4) return false;
   const int pad = ks / 2;

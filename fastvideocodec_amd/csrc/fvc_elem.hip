@@ -285,6 +285,79 @@ __global__ __launch_bounds__(kBlk) void k_gdn(const float* __restrict__ x, float
   }
 }
 
+// GDN / IGDN on the fp32 matrix cores. norm = conv1x1(x^2, gamma) + beta is a [32 px x 64] x
+// [64 x 64] product per 32-pixel group: 2 N-tiles x 32 v_mfma_f32_32x32x2_f32 (an exact fp32 FMA
+// chain per output). gamma^T fragments stay in 64 VGPRs for the whole kernel. Lane (p, h) loads
+// channels [32h, 32h+32) of pixel p (its A operand for all 32 MFMAs: MFMA s pairs channel s with
+// s+32), parks them in a per-wave LDS tile, and reads x back in the accumulator layout (lane =
+// channel, register = pixel) for the normalisation, so HBM sees x once and y once.
+constexpr int kGdnWaves = 4;
+constexpr int kGdnRow = 68;  // LDS row stride in floats (272 B = 16 x odd: conflict-free b128 writes)
+
+__global__ __launch_bounds__(64 * kGdnWaves) void k_gdn_mfma(const float* __restrict__ x, float* __restrict__ y,
+                                                          const float* __restrict__ beta,
+                                                          const float* __restrict__ gamma, size_t npix,
+                                                          int inverse) {
+  __shared__ float xt[kGdnWaves * 32 * kGdnRow];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int li = lane & 31, lh = lane >> 5;
+  float g0[32], g1[32];  // gamma^T[k = s + 32 lh][n = li (+32)] = gamma[n][k]
+#pragma unroll
+  for (int s = 0; s < 32; ++s) {
+    g0[s] = gamma[li * 64 + s + 32 * lh];
+    g1[s] = gamma[(32 + li) * 64 + s + 32 * lh];
+  }
+  const float b0 = beta[li], b1 = beta[32 + li];
+  float* xw = xt + wave * 32 * kGdnRow;
+  const size_t ngroups = (npix + 31) / 32;
+  // the next group's x is loaded while the current group's MFMAs run
+  float4 nx[8];
+  auto fetch = [&](size_t gi) {
+    const size_t p = gi * 32 + li;
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      nx[k] = p < npix ? reinterpret_cast<const float4*>(x + p * 64 + 32 * lh)[k] : make_float4(0.f, 0.f, 0.f, 0.f);
+  };
+  const size_t gstep = (size_t)gridDim.x * kGdnWaves;
+  size_t gi = (size_t)blockIdx.x * kGdnWaves + wave;
+  if (gi < ngroups) fetch(gi);
+  for (; gi < ngroups; gi += gstep) {
+    const size_t p0 = gi * 32;
+    float a[32];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float4 v = nx[k];
+      a[4 * k] = v.x; a[4 * k + 1] = v.y; a[4 * k + 2] = v.z; a[4 * k + 3] = v.w;
+      *reinterpret_cast<float4*>(xw + li * kGdnRow + 32 * lh + 4 * k) = v;
+    }
+    if (gi + gstep < ngroups) fetch(gi + gstep);
+    f32x16 acc0, acc1;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      acc0[r] = 0.f;
+      acc1[r] = 0.f;
+    }
+#pragma unroll
+    for (int s = 0; s < 32; ++s) {
+      const float sq = a[s] * a[s];
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(sq, g0[s], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(sq, g1[s], acc1, 0, 0, 0);
+    }
+    // accumulator layout: lane (li, lh), register r -> pixel q = (r&3) + 8(r>>2) + 4lh, channel li (+32)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int q = (r & 3) + 8 * (r >> 2) + 4 * lh;
+      if (p0 + q < npix) {
+        const float x0 = xw[q * kGdnRow + li], x1 = xw[q * kGdnRow + 32 + li];
+        const float n0 = sqrtf(acc0[r] + b0), n1 = sqrtf(acc1[r] + b1);
+        float* yo = y + (p0 + q) * 64;
+        yo[li] = inverse ? x0 * n0 : x0 / n0;
+        yo[32 + li] = inverse ? x1 * n1 : x1 / n1;
+      }
+    }
+  }
+}
+
 // ------------------------------------------------------------------ deterministic reductions
 template <int K>
 __device__ void block_reduce_store(double (&v)[K], double* out) {
@@ -505,8 +578,11 @@ int fvc_gdn_nhwc(const float* x, float* y, const float* beta, const float* gamma
                  int inverse, fvc_stream_t s) {
   if (!x || !y || !beta || !gamma || c != 64) return FVC_EINVAL;
   const size_t npix = (size_t)batch * h * w;
-  hipLaunchKernelGGL(k_gdn<64>, dim3(grid_for(npix)), dim3(kBlk), 0, (hipStream_t)s, x, y, beta, gamma, npix,
-                     inverse);
+  size_t nblk = ((npix + 31) / 32 + kGdnWaves - 1) / kGdnWaves;
+  if (nblk > 2048) nblk = 2048;
+  if (nblk < 1) nblk = 1;
+  hipLaunchKernelGGL(k_gdn_mfma, dim3((unsigned)nblk), dim3(64 * kGdnWaves), 0, (hipStream_t)s, x, y, beta, gamma,
+                     npix, inverse);
   FVC_CHECK_LAUNCH();
   return 0;
 }

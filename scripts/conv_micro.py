@@ -19,6 +19,15 @@ CASES = {
     "d5_64_quarter": (64, 64, 5, 2, True, 272, 480),
     "d5_96_64_16": (96, 64, 5, 2, True, 136, 240),
     "c7_32_16_full": (32, 16, 7, 1, False, 1088, 1920),
+    "c3_64_half": (64, 64, 3, 1, False, 544, 960),
+    "c3_128_quarter": (128, 128, 3, 1, False, 272, 480),
+    "c3_128_eighth": (128, 128, 3, 1, False, 136, 240),
+    "c7_8_32_full": (8, 32, 7, 1, False, 1088, 1920),
+    "c3_6_64_full": (6, 64, 3, 1, False, 1088, 1920),
+    "c3s2_128_half": (128, 128, 3, 2, False, 544, 960),
+    "c3_64_3_full": (64, 3, 3, 1, False, 1088, 1920),
+    "d5_64_3_half": (64, 3, 5, 2, True, 1088, 1920),
+    "c7_16_2_full": (16, 2, 7, 1, False, 1088, 1920),
 }
 
 ap = argparse.ArgumentParser()

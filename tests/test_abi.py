@@ -106,5 +106,6 @@ def test_x3_pack_splits_every_weight_once(geom):
 def test_x3_rejects_unsupported_layers():
     lib = _lib.load()
     assert lib.fvc_conv_x3_supported(2, 128, 3, 2, 0) == 0  # cin padded to 4: fp32 kernel
-    assert lib.fvc_conv_x3_supported(64, 3, 3, 1, 0) == 0   # cout <= 4: VALU small-N kernel
-    assert lib.fvc_conv_x3_wpack_bytes(64, 3, 3, 1, 0) == 0
+    assert lib.fvc_conv_x3_supported(16, 2, 7, 1, 0) == 0   # 7x7 cout <= 4: VALU small-N kernel
+    assert lib.fvc_conv_x3_wpack_bytes(16, 2, 7, 1, 0) == 0
+    assert lib.fvc_conv_x3_supported(64, 3, 3, 1, 0) == 1   # 3x3 cout <= 4: N padded to one MFMA tile
