@@ -9,7 +9,7 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libfvc.so")
+LIB_PATH = os.environ.get("FVC_LIB_PATH") or os.path.join(_HERE, "libfvc.so")  # override: experiments only
 
 c_int = ctypes.c_int
 c_float = ctypes.c_float

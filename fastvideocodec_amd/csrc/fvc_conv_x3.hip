@@ -46,6 +46,21 @@ typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 
 constexpr int kMaxTapsX = 49;
 
+// Accumulation scheme. Dual (default): two weight planes (hi, lo*2^11); the correction
+// products go to a second accumulator scaled by 2^-11 at the end. Single (-DFVC_X3_SINGLE,
+// experiment): three planes, hi, lo (unscaled: w*2^kw keeps it in fp16's normal range) and
+// hi*2^-11, all products in ONE accumulator (acc += xh*wh + xh*wl + xl_s*(wh*2^-11)), which
+// frees 64 VGPRs for a distance-2 operand prefetch. Measured (scripts/conv_micro.py, MI355X):
+// single is 8-13 % slower -- the 50 % larger weight stream costs more than the deeper prefetch
+// gains -- so dual ships.
+#ifdef FVC_X3_SINGLE
+constexpr bool kSingleAcc = true;
+#else
+constexpr bool kSingleAcc = false;
+#endif
+constexpr int kNPL = kSingleAcc ? 3 : 2;   // weight planes per (k-step, N-tile)
+constexpr int kFrag = 64 * kNPL;          // uint4 per (k-step, N-tile)
+
 __device__ int g_x3_overflow;
 
 struct X3Args {
@@ -99,7 +114,9 @@ __device__ __forceinline__ void split8(const float (&v)[8], h8& hi, h8& lo, floa
                        fmaxf(fmaxf(fabsf(v[4]), fabsf(v[5])), fmaxf(fabsf(v[6]), fabsf(v[7])))));
 }
 
-template <int CC, int WM, int WN, int NW, int IOP>
+// DBG (ablation builds only, scripts/gpu_x3_ablate.sh; 0 in the product): bit 0 no staging of
+// later chunks, bit 1 no weight loads in the k-loop, bit 2 no output stores, bit 3 no A LDS reads
+template <int CC, int WM, int WN, int NW, int IOP, int DBG = 0>
 __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(const X3Args a) {
   constexpr int C8 = CC / 8;
   constexpr int PSH = 2 * CC + 8;  // pixel stride in halves: 4*CC bytes + 16 -> 16 x odd bytes
@@ -187,9 +204,9 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(const X3Args a) {
 
   struct Ops {
     h8 ah[WM], al[WM];
-    uint4 bh[WN], bl[WN];
+    uint4 bh[WN], bl[WN], bd[kSingleAcc ? WN : 1];
   };
-  f32x16 acc[WM][WN], cor[WM][WN];
+  f32x16 acc[WM][WN], cor[WM][kSingleAcc ? 1 : WN];
   int buf = 0;  // LDS buffer holding the chunk being multiplied
   for (int tile = t_begin; tile < t_end; ++tile) {
 #pragma unroll
@@ -199,7 +216,7 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(const X3Args a) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           acc[m][n][r] = 0.f;
-          cor[m][n][r] = 0.f;
+          if constexpr (!kSingleAcc) cor[m][n][r] = 0.f;
         }
 
     // K loop over channel chunks. Two operand register sets (ping-pong, no copies). Each
@@ -214,8 +231,8 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(const X3Args a) {
       const bool last = ch + 1 == nch;
       const int s_tile = last ? tile + 1 : tile;
       const int s_ch = last ? 0 : ch + 1;
-      const bool stage_next = s_tile < t_end;
-      const uint4* wch = wcls + (size_t)ch * nq * a.ntp * 128;
+      const bool stage_next = (DBG & 1) ? false : s_tile < t_end;
+      const uint4* wch = wcls + (size_t)ch * nq * a.ntp * kFrag;
       // k-step q: lane half lh takes k8-block kb = 2q + lh = (tap kb / C8, octet kb % C8)
       auto load = [&](int q, Ops& op) {
         int toff;
@@ -228,14 +245,26 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(const X3Args a) {
         }
 #pragma unroll
         for (int m = 0; m < WM; ++m) {
-          op.ah[m] = *reinterpret_cast<const h8*>(cur + pix0 + m * pix_m + toff);
-          op.al[m] = *reinterpret_cast<const h8*>(cur + pix0 + m * pix_m + toff + CC);
+          if constexpr (DBG & 8) {
+            op.ah[m] = (h8)(_Float16)(toff & 7);
+            op.al[m] = op.ah[m];
+          } else {
+            op.ah[m] = *reinterpret_cast<const h8*>(cur + pix0 + m * pix_m + toff);
+            op.al[m] = *reinterpret_cast<const h8*>(cur + pix0 + m * pix_m + toff + CC);
+          }
         }
-        const uint4* wk = wch + ((size_t)q * a.ntp + nt0) * 128 + lane;
+        const uint4* wk = wch + ((size_t)q * a.ntp + nt0) * kFrag + lane;
 #pragma unroll
         for (int n = 0; n < WN; ++n) {
-          op.bh[n] = wk[n * 128];
-          op.bl[n] = wk[n * 128 + 64];
+          if constexpr (DBG & 2) {
+            op.bh[n] = make_uint4(q, n, 1, 2);
+            op.bl[n] = op.bh[n];
+            if constexpr (kSingleAcc) op.bd[n] = op.bh[n];
+          } else {
+            op.bh[n] = wk[n * kFrag];
+            op.bl[n] = wk[n * kFrag + 64];
+            if constexpr (kSingleAcc) op.bd[n] = wk[n * kFrag + 128];
+          }
         }
       };
       auto mfmas = [&](const Ops& op) {
@@ -245,9 +274,16 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(const X3Args a) {
           for (int n = 0; n < WN; ++n) {
             const h8 wh = __builtin_bit_cast(h8, op.bh[n]);
             const h8 wl = __builtin_bit_cast(h8, op.bl[n]);
-            acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(op.ah[m], wh, acc[m][n], 0, 0, 0);
-            cor[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(op.ah[m], wl, cor[m][n], 0, 0, 0);
-            cor[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(op.al[m], wh, cor[m][n], 0, 0, 0);
+            if constexpr (kSingleAcc) {
+              const h8 wd = __builtin_bit_cast(h8, op.bd[n]);
+              acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(op.ah[m], wh, acc[m][n], 0, 0, 0);
+              acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(op.ah[m], wl, acc[m][n], 0, 0, 0);
+              acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(op.al[m], wd, acc[m][n], 0, 0, 0);
+            } else {
+              acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(op.ah[m], wh, acc[m][n], 0, 0, 0);
+              cor[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(op.ah[m], wl, cor[m][n], 0, 0, 0);
+              cor[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(op.al[m], wh, cor[m][n], 0, 0, 0);
+            }
           }
       };
       auto half_plain = [&](int q, const Ops& use, Ops& nxt_ops) {
@@ -265,29 +301,75 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(const X3Args a) {
         __builtin_amdgcn_sched_barrier(0);
         store(nxt, st);
       };
-      Ops S0, S1;
-      load(0, S0);
-      // staging items of the next chunk are spread evenly over the k-step pairs (one per staged
-      // pair) so their VALU work interleaves with MFMA-only steps instead of bunching up at the
-      // chunk start, where every wave would be VALU-bound at once
-      const int npair = nq >> 1;
-      const int nst = stage_next ? min(nstage, npair) : 0;
-      const int spread = nst ? max(1, npair / nst) : 1;
-      int q = 0, staged = 0;
-      for (; staged < nst; ++staged) {
-        half_stage(tid + staged * NT, q, S0, S1);
-        half_plain(q + 1, S1, S0);
-        q += 2;
-        for (int r = 1; r < spread; ++r, q += 2) {
+      int staged = 0;
+      if constexpr (kSingleAcc) {
+        // prefetch distance 2 (the single accumulator leaves room for three operand sets): step
+        // q multiplies S[q % 3] and loads k-step q+2 into the set step q-1 just finished with
+        auto step_plain = [&](int q, const Ops& use, Ops& nxt_ops) {
+          load(q + 2 < nq ? q + 2 : nq - 1, nxt_ops);
+          __builtin_amdgcn_sched_barrier(0);
+          mfmas(use);
+          __builtin_amdgcn_sched_barrier(0);
+        };
+        auto step_stage = [&](int item, int q, const Ops& use, Ops& nxt_ops) {
+          load(q + 2 < nq ? q + 2 : nq - 1, nxt_ops);
+          Stage st;
+          fetch(item, s_tile, s_ch, st);
+          __builtin_amdgcn_sched_barrier(0);
+          mfmas(use);
+          __builtin_amdgcn_sched_barrier(0);
+          store(nxt, st);
+        };
+        Ops S0, S1, S2;
+        load(0, S0);
+        load(nq > 1 ? 1 : 0, S1);
+        const int ntri = nq / 3;
+        const int nst = stage_next ? min(nstage, ntri) : 0;
+        const int spread = nst ? max(1, ntri / nst) : 1;
+        int q = 0;
+        for (; staged < nst; ++staged) {
+          step_stage(tid + staged * NT, q, S0, S2);
+          step_plain(q + 1, S1, S0);
+          step_plain(q + 2, S2, S1);
+          q += 3;
+          for (int r = 1; r < spread; ++r, q += 3) {
+            step_plain(q, S0, S2);
+            step_plain(q + 1, S1, S0);
+            step_plain(q + 2, S2, S1);
+          }
+        }
+        for (; q + 2 < nq; q += 3) {
+          step_plain(q, S0, S2);
+          step_plain(q + 1, S1, S0);
+          step_plain(q + 2, S2, S1);
+        }
+        if (q < nq) mfmas(S0);
+        if (q + 1 < nq) mfmas(S1);
+      } else {
+        Ops S0, S1;
+        load(0, S0);
+        // staging items of the next chunk are spread evenly over the k-step pairs (one per staged
+        // pair) so their VALU work interleaves with MFMA-only steps instead of bunching up at the
+        // chunk start, where every wave would be VALU-bound at once
+        const int npair = nq >> 1;
+        const int nst = stage_next ? min(nstage, npair) : 0;
+        const int spread = nst ? max(1, npair / nst) : 1;
+        int q = 0;
+        for (; staged < nst; ++staged) {
+          half_stage(tid + staged * NT, q, S0, S1);
+          half_plain(q + 1, S1, S0);
+          q += 2;
+          for (int r = 1; r < spread; ++r, q += 2) {
+            half_plain(q, S0, S1);
+            half_plain(q + 1, S1, S0);
+          }
+        }
+        for (; q + 1 < nq; q += 2) {
           half_plain(q, S0, S1);
           half_plain(q + 1, S1, S0);
         }
+        if (nq & 1) mfmas(S0);
       }
-      for (; q + 1 < nq; q += 2) {
-        half_plain(q, S0, S1);
-        half_plain(q + 1, S1, S0);
-      }
-      if (nq & 1) mfmas(S0);
       if (stage_next) {
         for (int qs = staged; qs < nstage; ++qs) {
           Stage st;
@@ -321,7 +403,9 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(const X3Args a) {
         float v[16];
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const float t = fmaf(cor[m][n][r], a.osc_c, acc[m][n][r] * a.osc) + bj;
+          float t;
+          if constexpr (kSingleAcc) t = acc[m][n][r] * a.osc + bj;
+          else t = fmaf(cor[m][n][r], a.osc_c, acc[m][n][r] * a.osc) + bj;
           v[r] = fmaxf(t, t * a.act_slope);
         }
         if (a.res && j < a.coutp) {  // lanes past coutp (cout <= 4 layers) must not read: OOB
@@ -340,7 +424,11 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(const X3Args a) {
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
             const int dx = (r & 3) + 8 * (r >> 2);
-            if (full_w || qx0 + 4 * lh + dx < a.Wq) yr[dx * pstride] = real ? v[r] : 0.f;
+            if constexpr (DBG & 4) {
+              asm volatile("" ::"v"(v[r]));
+            } else {
+              if (full_w || qx0 + 4 * lh + dx < a.Wq) yr[dx * pstride] = real ? v[r] : 0.f;
+            }
           }
         }
       }
@@ -453,7 +541,7 @@ static bool x3_cfg(int cin, int cout, int ks, int stride, int transposed, X3Cfg&
   for (int cl = 0; cl < c.nclass; ++cl) {
     c.nks[cl] = fvc_cdiv(c.ntaps[cl] * (c.cc / 8), 2);
     c.wcls[cl] = off;
-    off += (long long)c.nchunks * c.nks[cl] * c.ntp * 128;  // 128 uint4 per (k-step, N-tile)
+    off += (long long)c.nchunks * c.nks[cl] * c.ntp * kFrag;  // kFrag uint4 per (k-step, N-tile)
   }
   c.wtotal = off;
   return true;
@@ -480,14 +568,41 @@ static int x3_kw(const float* w, size_t n) {
   return kw < -100 ? -100 : (kw > 100 ? 100 : kw);
 }
 
-template <int CC, int WM, int WN, int IOP>
-static int x3_launch_t(const X3Args& a, dim3 grid, size_t lds, hipStream_t s) {
+template <int CC, int WM, int WN, int IOP, int DBG>
+static int x3_launch_d(const X3Args& a, dim3 grid, size_t lds, hipStream_t s) {
   if (lds > 64 * 1024)
-    (void)hipFuncSetAttribute((const void*)conv_x3_kernel<CC, WM, WN, 8, IOP>,
+    (void)hipFuncSetAttribute((const void*)conv_x3_kernel<CC, WM, WN, 8, IOP, DBG>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL((conv_x3_kernel<CC, WM, WN, 8, IOP>), grid, dim3(8 * 64), lds, s, a);
+  hipLaunchKernelGGL((conv_x3_kernel<CC, WM, WN, 8, IOP, DBG>), grid, dim3(8 * 64), lds, s, a);
   FVC_CHECK_LAUNCH();
   return 0;
+}
+
+#ifdef FVC_X3_ABLATE
+static int x3_dbg() {
+  static int d = -1;
+  if (d < 0) d = env_int("FVC_X3_DBG", 0);
+  return d;
+}
+#endif
+
+template <int CC, int WM, int WN, int IOP>
+static int x3_launch_t(const X3Args& a, dim3 grid, size_t lds, hipStream_t s) {
+#ifdef FVC_X3_ABLATE
+  if (CC == 16 && WM == 2 && WN == 2 && IOP == 0) {
+    switch (x3_dbg()) {
+      case 1: return x3_launch_d<CC, WM, WN, IOP, 1>(a, grid, lds, s);
+      case 2: return x3_launch_d<CC, WM, WN, IOP, 2>(a, grid, lds, s);
+      case 4: return x3_launch_d<CC, WM, WN, IOP, 4>(a, grid, lds, s);
+      case 8: return x3_launch_d<CC, WM, WN, IOP, 8>(a, grid, lds, s);
+      case 3: return x3_launch_d<CC, WM, WN, IOP, 3>(a, grid, lds, s);
+      case 15: return x3_launch_d<CC, WM, WN, IOP, 15>(a, grid, lds, s);
+      case 11: return x3_launch_d<CC, WM, WN, IOP, 11>(a, grid, lds, s);
+      default: break;
+    }
+  }
+#endif
+  return x3_launch_d<CC, WM, WN, IOP, 0>(a, grid, lds, s);
 }
 
 template <int CC, int WM, int WN>
@@ -627,16 +742,20 @@ int fvc_conv_x3_pack_weight(const float* w, void* wp, float* osc_out, int cin, i
             const int j = nt * 32 + li;
             if (t >= c.ntaps[cl] || j >= cout) continue;
             const int ky = c.tky[cl][t], kx = c.tkx[cl][t];
-            const size_t frag = ((((size_t)c.wcls[cl] + (((size_t)ch * c.nks[cl] + q) * c.ntp + nt) * 128)) + lane) * 8;
+            const size_t frag = ((((size_t)c.wcls[cl] + (((size_t)ch * c.nks[cl] + q) * c.ntp + nt) * kFrag)) + lane) * 8;
             for (int e = 0; e < 8; ++e) {
               const int ci = ch * c.cc + o * 8 + e;
               if (ci >= cin) continue;
               const float v = (transposed ? w[(((size_t)ci * cout + j) * ks + ky) * ks + kx]
                                           : w[(((size_t)j * cin + ci) * ks + ky) * ks + kx]) * sc;
               const _Float16 hi = (_Float16)v;
-              const _Float16 lo = (_Float16)((v - (float)hi) * 2048.f);
-              out[frag + e] = hi;              // plane 0 (hi): lanes 0..63
-              out[frag + 64 * 8 + e] = lo;     // plane 1 (lo): +64 lanes
+              out[frag + e] = hi;  // plane 0 (hi): lanes 0..63
+              if (kSingleAcc) {
+                out[frag + 64 * 8 + e] = (_Float16)(v - (float)hi);              // plane 1: lo, unscaled
+                out[frag + 128 * 8 + e] = (_Float16)((float)hi * (1.f / 2048.f));  // plane 2: hi * 2^-11
+              } else {
+                out[frag + 64 * 8 + e] = (_Float16)((v - (float)hi) * 2048.f);   // plane 1: lo * 2^11
+              }
             }
           }
   return 0;
