@@ -67,6 +67,24 @@ def cpu_baseline(H, W, frames_np):
             "seconds": round(dt, 2)}
 
 
+def load_pmc_traffic(H, W):
+    """HBM bytes per conv_x3_kernel launch from the committed rocprofv3 FETCH_SIZE/WRITE_SIZE passes
+    over `bench.py --serial` (profiles/r1/x3_traffic.json, written by scripts/rocprof_summary.py;
+    FETCH_SIZE doubled per MI355X_MICROARCH.md's gfx950 correction). PMC passes serialise every
+    dispatch and cannot run inside the timed region, so the figure is the profiled one."""
+    path = os.path.join(REPO, "profiles", "r1", "x3_traffic.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return {}
+    if d.get("height") != H or d.get("width") != W:
+        return {}
+    return {"hbm_bytes_per_launch": d.get("hbm_bytes_per_launch"),
+            "source": f"profiles/r1/x3_traffic.json (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, "
+                      f"{d.get('launches')} launches)"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -123,6 +141,7 @@ def main():
         encode_decode_gop(model, frames, overlap=False)
     conv_ms, conv_flops, n_launch = timer.collect()
     x3_ms, x3_flops, x3_launch = timer.collect(x3=True)
+    x3_bytes = timer.collect_bytes(x3=True)
     if args.breakdown and rank == 0:
         agg = timer.breakdown()
         for k, (n, ms, fl) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
@@ -131,7 +150,7 @@ def main():
     # ---- verification + quality, outside the timed region
     from fastvideocodec_amd import kernels as K
     K.x3_overflow(reset=True)
-    bss, decoded, sses, encs = encode_decode_gop(model, frames, check=True)
+    bss, decoded, sses, encs = encode_decode_gop(model, frames, check=True, overlap=overlap)
     torch.cuda.synchronize()
     x3_overflow = K.x3_overflow(reset=True)
     bitexact = all(torch.equal(a, b) for a, b in zip(decoded, encs))
@@ -150,6 +169,7 @@ def main():
     bytes_all = float(allst[:, 1].sum())
     psnr_all = float(np.mean(allst[:, 2]))
 
+    pmc_traffic = load_pmc_traffic(args.height, args.width)
     pframes = args.steps * G * (args.gop - 1) * world
     value = pframes / dt_max
     nfr = G * (args.gop - 1)
@@ -172,7 +192,12 @@ def main():
                    "gops_per_gpu": G, "frames_counted": "P-frames only (I-frame pass-through)",
                    "parallelism": f"gop-shard x{world}"},
         "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": F16_MFMA_PEAK_TFLOPS,
-                     "unit": "TFLOP/s", "frac": round(achieved / F16_MFMA_PEAK_TFLOPS, 4), "traffic": None,
+                     "unit": "TFLOP/s", "frac": round(achieved / F16_MFMA_PEAK_TFLOPS, 4),
+                     "traffic": pmc_traffic.get("hbm_bytes_per_launch"),
+                     "traffic_source": pmc_traffic.get("source"),
+                     "avg_launch_us": round(x3_ms * 1e3 / x3_launch, 2) if x3_launch else None,
+                     "algorithmic_bytes_per_launch": round(x3_bytes / x3_launch) if x3_launch else None,
+                     "algorithmic_gbps": round(x3_bytes / (x3_ms * 1e-3) / 1e9, 1) if x3_ms else None,
                      "kernel": "conv_x3_kernel (split-precision fp16x3 implicit-GEMM conv/deconv): all its launches",
                      "achieved_is": "algorithmic fp32-conv FLOP (2 x MAC) / kernel time; the kernel issues 3 f16 "
                                     "MFMAs per MAC, so its ceiling in these units is peak/3",

@@ -208,10 +208,14 @@ class PackedConv:
                       W, self.cin, self.cout, self.ksize, self.stride, in_op, act, post, stream_handle())
         if timer is not None:
             ev1.record()
+            # algorithmic HBM bytes: input + weights + output (+ residual), each touched once
+            nbytes = 4 * (x.numel() + y.numel() * (2 if res is not None else 1)) + self.wpack.numel() * \
+                self.wpack.element_size()
             timer.records.append((ev0, ev1, profiling.conv_flops(self.cin, self.cout, self.ksize, self.stride,
                                                                  self.transposed, B, H, W),
                                   f"{'deconv' if self.transposed else 'conv'}{self.ksize}s{self.stride} "
-                                  f"{self.cin}->{self.cout} @{H}x{W}{' x3' if self.x3 else ''}", self.x3))
+                                  f"{self.cin}->{self.cout} @{H}x{W}{' x3' if self.x3 else ''}", self.x3,
+                                  nbytes))
         return y
 
 

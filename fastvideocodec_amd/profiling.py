@@ -42,6 +42,11 @@ class KernelTimer:
         fl = sum(r[2] for r in rs)
         return ms, fl, len(rs)
 
+    def collect_bytes(self, x3=None):
+        """Algorithmic HBM bytes (input + packed weights + output + residual) of the launches
+        ``collect(x3)`` counts."""
+        return sum(r[5] for r in self.records if len(r) > 5 and (x3 is None or r[4] == x3))
+
     def breakdown(self):
         """Per-geometry aggregate: {key: [launches, ms, flops]} (keys recorded by the caller)."""
         torch.cuda.synchronize()

@@ -1,36 +1,79 @@
 """Summarise a rocprofv3 --kernel-trace --stats run of `bench.py --serial` per P-frame and
-(optionally) the FETCH_SIZE/WRITE_SIZE PMC passes, for comparison with bench.py's roofline.
+(optionally) the FETCH_SIZE/WRITE_SIZE PMC passes over the same command, for comparison with
+bench.py's roofline object (which times conv_x3_kernel with HIP events on its stream).
 
-usage: python scripts/rocprof_summary.py <stats_csv> <n_pframes_total> [fetch_csv write_csv]
+usage: python scripts/rocprof_summary.py <stats_csv> <n_pframes_total>
+           [--fetch fetch_counter_collection.csv --write write_counter_collection.csv
+            --json-out profiles/r1/x3_traffic.json --height 1080 --width 1920]
 """
+import argparse
 import csv
-import sys
+import json
 
 CONV_PREFIXES = ("conv_x3_kernel", "conv_mfma_f32_kernel", "conv_mfma_pipe_kernel", "deconv2_mfma_f32_kernel",
                  "conv_smalln_f32_kernel")
+X3 = "conv_x3_kernel"
 
 
 def is_conv(name):
     return any(p in name for p in CONV_PREFIXES)
 
 
+def pmc_per_dispatch(path, counter, sub):
+    """{dispatch_id: value in bytes} for kernels whose name contains `sub` (counter unit: KiB)."""
+    out = {}
+    for r in csv.DictReader(open(path)):
+        if r.get("Counter_Name") == counter and sub in r["Kernel_Name"]:
+            d = int(r["Dispatch_Id"])
+            out[d] = out.get(d, 0.0) + float(r["Counter_Value"]) * 1024.0
+    return out
+
+
 def main():
-    stats, nframes = sys.argv[1], int(sys.argv[2])
-    rows = list(csv.DictReader(open(stats)))
+    ap = argparse.ArgumentParser()
+    ap.add_argument("stats")
+    ap.add_argument("nframes", type=int)
+    ap.add_argument("--fetch")
+    ap.add_argument("--write")
+    ap.add_argument("--json-out")
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--width", type=int, default=1920)
+    a = ap.parse_args()
+    nframes = a.nframes
+    rows = list(csv.DictReader(open(a.stats)))
     tot = sum(float(r["TotalDurationNs"]) for r in rows)
     conv = sum(float(r["TotalDurationNs"]) for r in rows if is_conv(r["Name"]))
     calls = sum(int(r["Calls"]) for r in rows if is_conv(r["Name"]))
+    x3_ns = sum(float(r["TotalDurationNs"]) for r in rows if X3 in r["Name"])
+    x3_calls = sum(int(r["Calls"]) for r in rows if X3 in r["Name"])
     print(f"all kernels: {tot / 1e6:.2f} ms total, {tot / 1e6 / nframes:.3f} ms per P-frame")
     print(f"conv family: {conv / 1e6:.2f} ms total over {calls} launches, {conv / 1e6 / nframes:.3f} ms per P-frame")
+    if x3_calls:
+        print(f"{X3} (all instantiations): {x3_calls} launches, avg {x3_ns / x3_calls / 1e3:.2f} us, "
+              f"{x3_ns / 1e6 / nframes:.3f} ms per P-frame")
     print("top kernels (ms per P-frame):")
     for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"]))[:15]:
-        print(f"  {float(r['TotalDurationNs']) / 1e6 / nframes:8.3f}  n/frame={int(r['Calls']) / nframes:6.1f}  {r['Name'][:100]}")
-    if len(sys.argv) > 4:
-        for label, path, col in (("FETCH", sys.argv[3], "FETCH_SIZE"), ("WRITE", sys.argv[4], "WRITE_SIZE")):
-            rr = list(csv.DictReader(open(path)))
-            kb = sum(float(r["Counter_Value"]) for r in rr if r.get("Counter_Name") == col and is_conv(r["Kernel_Name"]))
-            corr = 2.0 if label == "FETCH" else 1.0  # gfx950: FETCH_SIZE reads 1/2 of wide streaming reads
-            print(f"conv {label}: {kb * corr * 1024 / nframes / 1e9:.3f} GB per P-frame (corrected x{corr:g})")
+        print(f"  {float(r['TotalDurationNs']) / 1e6 / nframes:8.3f}  n/frame={int(r['Calls']) / nframes:6.1f}  "
+              f"{r['Name'][:100]}")
+    if a.fetch and a.write:
+        # gfx950: FETCH_SIZE tallies 128-B requests at 64 B -> x2 (MI355X_MICROARCH.md, HBM section);
+        # WRITE_SIZE exact for 16-B-per-lane stores (the x3 epilogue stores float4)
+        f = pmc_per_dispatch(a.fetch, "FETCH_SIZE", X3)
+        w = pmc_per_dispatch(a.write, "WRITE_SIZE", X3)
+        fb = 2.0 * sum(f.values()) / max(1, len(f))
+        wb = sum(w.values()) / max(1, len(w))
+        fc = 2.0 * sum(v for k, v in pmc_per_dispatch(a.fetch, "FETCH_SIZE", "").items()) / 1e9
+        print(f"{X3}: {len(f)} dispatches with FETCH_SIZE, {len(w)} with WRITE_SIZE; per launch "
+              f"fetch {fb / 1e6:.3f} MB (x2 corrected), write {wb / 1e6:.3f} MB")
+        print(f"all kernels FETCH (x2): {fc:.3f} GB")
+        if a.json_out:
+            with open(a.json_out, "w") as fo:
+                json.dump({"kernel": X3, "height": a.height, "width": a.width, "launches": len(f),
+                           "fetch_bytes_per_launch": round(fb), "write_bytes_per_launch": round(wb),
+                           "hbm_bytes_per_launch": round(fb + wb),
+                           "avg_launch_us_kernel_trace": round(x3_ns / x3_calls / 1e3, 2) if x3_calls else None,
+                           "correction": "FETCH_SIZE x2 (gfx950 wide-read tally), WRITE_SIZE x1"}, fo, indent=1)
+            print("wrote", a.json_out)
 
 
 if __name__ == "__main__":
