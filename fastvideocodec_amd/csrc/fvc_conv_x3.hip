@@ -128,6 +128,7 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(const X3Args a) {
   const int tile_h = (a.ir * a.ic * PSH + 7) & ~7;
   _Float16* const tile0 = smh + 128;  // two buffers at tile0 and tile0 + tile_h (LDS pointers;
                                       // no pointer array, which would degrade them to flat)
+  float* const sbias = reinterpret_cast<float*>(smh);  // [WN * 32] bias of this block's N-tiles
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -193,6 +194,10 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(const X3Args a) {
     Stage st;
     fetch(e, t_begin, 0, st);
     store(tile0, st);
+  }
+  if (tid < WN * 32) {
+    const int j = nt0 * 32 + tid;
+    sbias[tid] = j < a.cout ? a.bias[j] : 0.f;
   }
 
   const int pix0 = (((wave * WM) * a.sin) * a.ic + li) * PSH;  // strip m adds m * pix_m
@@ -274,15 +279,18 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(const X3Args a) {
           for (int n = 0; n < WN; ++n) {
             const h8 wh = __builtin_bit_cast(h8, op.bh[n]);
             const h8 wl = __builtin_bit_cast(h8, op.bl[n]);
+            // weights as the A (row) operand, pixels as B: the 32x32 result is channel x pixel,
+            // so each lane ends up with 4 consecutive channels of one pixel per register group
+            // (16-B epilogue stores)
             if constexpr (kSingleAcc) {
               const h8 wd = __builtin_bit_cast(h8, op.bd[n]);
-              acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(op.ah[m], wh, acc[m][n], 0, 0, 0);
-              acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(op.ah[m], wl, acc[m][n], 0, 0, 0);
-              acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(op.al[m], wd, acc[m][n], 0, 0, 0);
+              acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wh, op.ah[m], acc[m][n], 0, 0, 0);
+              acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wl, op.ah[m], acc[m][n], 0, 0, 0);
+              acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wd, op.al[m], acc[m][n], 0, 0, 0);
             } else {
-              acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(op.ah[m], wh, acc[m][n], 0, 0, 0);
-              cor[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(op.ah[m], wl, cor[m][n], 0, 0, 0);
-              cor[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(op.al[m], wh, cor[m][n], 0, 0, 0);
+              acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wh, op.ah[m], acc[m][n], 0, 0, 0);
+              cor[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wl, op.ah[m], cor[m][n], 0, 0, 0);
+              cor[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wh, op.al[m], cor[m][n], 0, 0, 0);
             }
           }
       };
@@ -382,53 +390,49 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(const X3Args a) {
     }
 
     // epilogue of this tile (its global stores drain while the next tile's k-loop runs).
-    // Lane (li, lh) holds output channel j = N-tile*32 + li of pixels qx0 + 4lh + {0..3, 8..11,
-    // 16..19, 24..27} (register r -> pixel (r&3) + 8(r>>2) + 4lh). Activation as one max:
-    // relu = max(v, 0*v), lrelu = max(v, 0.1*v), none = max(v, 1*v).
+    // Lane (li, lh) holds pixel qx0 + li of strip m; register group g (r = 4g..4g+3) holds output
+    // channels N-tile*32 + 8g + 4lh + {0..3} -> one 16-B store (and residual load) per group.
+    // Activation as one max: relu = max(v, 0*v), lrelu = max(v, 0.1*v), none = max(v, 1*v).
     const int qy0 = (tile / tiles_x) * TH, qx0 = (tile % tiles_x) * TW;
-    const bool full_w = qx0 + TW <= a.Wq;
-    const int pstride = a.sout * a.coutp;  // output floats per virtual column
+    const bool px_ok = qx0 + li < a.Wq;
 #pragma unroll
     for (int n = 0; n < WN; ++n) {
-      const int j = (nt0 + n) * 32 + li;
-      const bool real = j < a.cout;
-      const float bj = real ? a.bias[j < a.cout ? j : 0] : 0.f;
 #pragma unroll
       for (int m = 0; m < WM; ++m) {
         const int qy = qy0 + wave * WM + m;
         if (qy >= a.Hq || (nt0 + n) * 32 >= a.coutp) continue;  // wave-uniform
-        const size_t row = (((size_t)b * a.Ho + qy * a.sout + a.oy0[cls]) * a.Wo + a.ox0[cls] +
-                            (size_t)(qx0 + 4 * lh) * a.sout) * a.coutp + j;
-        float* yr = a.y + row;
-        float v[16];
+        const size_t prow = (((size_t)b * a.Ho + qy * a.sout + a.oy0[cls]) * a.Wo + a.ox0[cls] +
+                             (size_t)(qx0 + li) * a.sout) * a.coutp;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          float t;
-          if constexpr (kSingleAcc) t = acc[m][n][r] * a.osc + bj;
-          else t = fmaf(cor[m][n][r], a.osc_c, acc[m][n][r] * a.osc) + bj;
-          v[r] = fmaxf(t, t * a.act_slope);
-        }
-        if (a.res && j < a.coutp) {  // lanes past coutp (cout <= 4 layers) must not read: OOB
-          const float* rr = a.res + row;
+        for (int g = 0; g < 4; ++g) {
+          const int jl = 8 * g + 4 * lh;       // channel within the N-tile
+          const int j0 = (nt0 + n) * 32 + jl;  // first of this lane's 4 channels
+          if (j0 >= a.coutp) continue;         // cout <= 4 layers: only g = 0, lh = 0
+          const float4 bj = *reinterpret_cast<const float4*>(sbias + n * 32 + jl);
+          const float bb[4] = {bj.x, bj.y, bj.z, bj.w};
+          float v[4];
 #pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int dx = (r & 3) + 8 * (r >> 2);
-            if (full_w || qx0 + 4 * lh + dx < a.Wq) v[r] += rr[dx * pstride];
+          for (int i = 0; i < 4; ++i) {
+            const int r = 4 * g + i;
+            float t;
+            if constexpr (kSingleAcc) t = acc[m][n][r] * a.osc + bb[i];
+            else t = fmaf(cor[m][n][r], a.osc_c, acc[m][n][r] * a.osc) + bb[i];
+            v[i] = fmaxf(t, t * a.act_slope);
           }
-        }
-        if (a.post_op == FVC_POST_EXP) {
+          if (a.res && px_ok) {
+            const float4 rv = *reinterpret_cast<const float4*>(a.res + prow + j0);
+            v[0] += rv.x; v[1] += rv.y; v[2] += rv.z; v[3] += rv.w;
+          }
+          if (a.post_op == FVC_POST_EXP) {
 #pragma unroll
-          for (int r = 0; r < 16; ++r) v[r] = expf(v[r]);
-        }
-        if (j < a.coutp) {
+            for (int i = 0; i < 4; ++i) v[i] = expf(v[i]);
+          }
 #pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int dx = (r & 3) + 8 * (r >> 2);
-            if constexpr (DBG & 4) {
-              asm volatile("" ::"v"(v[r]));
-            } else {
-              if (full_w || qx0 + 4 * lh + dx < a.Wq) yr[dx * pstride] = real ? v[r] : 0.f;
-            }
+          for (int i = 0; i < 4; ++i) v[i] = j0 + i < a.cout ? v[i] : 0.f;  // pad channels = 0
+          if constexpr (DBG & 4) {
+            asm volatile("" ::"v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]));
+          } else {
+            if (px_ok) *reinterpret_cast<float4*>(a.y + prow + j0) = make_float4(v[0], v[1], v[2], v[3]);
           }
         }
       }
