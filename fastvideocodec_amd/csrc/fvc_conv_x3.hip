@@ -82,10 +82,14 @@ struct X3Args {
   int ntaps[4];
   int oy0[4], ox0[4];
   long long wcls[4];               // uint4 offset of each class in the pack
+  int ps;                          // LDS plane stride (halves): 8 x (pixels rounded to 8 mod 16)
+  int bq;                          // BL: uint4 per LDS weight buffer (max k-steps x WN x kFrag)
+  unsigned y_bytes;                // bytes of y (and res): < 4 GB - 256, the buffer range
   int toff[4][kMaxTapsX + 1];      // LDS offset (halves) of each tap's window; 0 past ntaps
 };
 
 typedef float f2v __attribute__((ext_vector_type(2)));
+typedef unsigned v4u __attribute__((ext_vector_type(4)));
 typedef _Float16 h2v __attribute__((ext_vector_type(2)));
 
 template <int IOP>
@@ -116,19 +120,21 @@ __device__ __forceinline__ void split8(const float (&v)[8], h8& hi, h8& lo, floa
 
 // DBG (ablation builds only, scripts/gpu_x3_ablate.sh; 0 in the product): bit 0 no staging of
 // later chunks, bit 1 no weight loads in the k-loop, bit 2 no output stores, bit 3 no A LDS reads
-template <int CC, int WM, int WN, int NW, int IOP, int DBG = 0>
+template <int CC, int WM, int WN, int NW, int IOP, int BL, int DBG = 0>
 __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(const X3Args a) {
   constexpr int C8 = CC / 8;
-  constexpr int PSH = 2 * CC + 8;  // pixel stride in halves: 4*CC bytes + 16 -> 16 x odd bytes
+  static_assert(!(kSingleAcc && BL), "weights-in-LDS path is dual-accumulator only");
   constexpr int TH = NW * WM;
   constexpr int TW = 32;
   constexpr int NT = NW * 64;
 
   extern __shared__ __attribute__((aligned(16))) _Float16 smh[];
-  const int tile_h = (a.ir * a.ic * PSH + 7) & ~7;
+  const int tile_h = 2 * C8 * a.ps;  // halves per A buffer: 2*C8 planes (hi octets, lo octets)
   _Float16* const tile0 = smh + 128;  // two buffers at tile0 and tile0 + tile_h (LDS pointers;
                                       // no pointer array, which would degrade them to flat)
   float* const sbias = reinterpret_cast<float*>(smh);  // [WN * 32] bias of this block's N-tiles
+  // BL: two weight buffers after the A buffers, each [k-step][N-tile][hi|lo][lane] uint4
+  _Float16* const wlds0 = tile0 + 2 * tile_h;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -161,10 +167,11 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(const X3Args a) {
   struct Stage {
     float4 v0, v1;
     int dst;
-    bool inb;
+    bool inb, ok;
   };
   auto fetch = [&](int e, int tile, int ch, Stage& st) {
-    e = e < tile_items ? e : tile_items - 1;  // duplicates rewrite the same value: benign
+    st.ok = e < tile_items;  // past the end: loads of a clamped index, no LDS write
+    e = st.ok ? e : tile_items - 1;
     const int o = e & (C8 - 1);
     const int p = e / C8;
     const int r = (int)(((float)p + 0.5f) * a.inv_ic);  // exact: p < 2^14, ic <= 128
@@ -178,7 +185,7 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(const X3Args a) {
     st.v0 = *reinterpret_cast<const float4*>(src);
     st.v1 = *reinterpret_cast<const float4*>(src + 4);
     const int cpos = hf ? ((c & 1) * hf + (c >> 1)) : c;
-    st.dst = (r * a.ic + cpos) * PSH + o * 8;
+    st.dst = o * a.ps + (r * a.ic + cpos) * 8;  // plane o (hi), pixel-minor
   };
   auto store = [&](_Float16* t, const Stage& st) {
     float v[8] = {st.v0.x, st.v0.y, st.v0.z, st.v0.w, st.v1.x, st.v1.y, st.v1.z, st.v1.w};
@@ -186,8 +193,23 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(const X3Args a) {
     for (int i = 0; i < 8; ++i) v[i] = st.inb ? in_op_t<IOP>(v[i]) : 0.f;
     h8 hi, lo;
     split8(v, hi, lo, mx);
-    *reinterpret_cast<h8*>(t + st.dst) = hi;
-    *reinterpret_cast<h8*>(t + st.dst + CC) = lo;
+    if (st.ok) {
+      *reinterpret_cast<h8*>(t + st.dst) = hi;
+      *reinterpret_cast<h8*>(t + st.dst + C8 * a.ps) = lo;
+    }
+  };
+  // BL: one weight staging item = one uint4 of the next chunk's [k-step][N-tile][hi|lo][lane]
+  // block slice (contiguous per k-step: N-tiles nt0..nt0+WN-1 are adjacent in the pack)
+  const int bitems = nq * WN * kFrag;
+  const int nbstage = BL ? (bitems + NT - 1) / NT : 0;
+  auto bfetch = [&](int i, int ch, uint4& v) {
+    i = i < bitems ? i : bitems - 1;
+    const int q = i / (WN * kFrag);
+    const int rem = i - q * (WN * kFrag);
+    v = wcls[((size_t)ch * nq + q) * a.ntp * kFrag + nt0 * kFrag + rem];
+  };
+  auto bstore = [&](_Float16* wb, int i, const uint4& v) {
+    if (i < bitems) *reinterpret_cast<uint4*>(wb + (size_t)i * 8) = v;
   };
 
   for (int e = tid; e < tile_items; e += NT) {
@@ -195,13 +217,20 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(const X3Args a) {
     fetch(e, t_begin, 0, st);
     store(tile0, st);
   }
+  if constexpr (BL != 0) {
+    for (int i = tid; i < bitems; i += NT) {
+      uint4 v;
+      bfetch(i, 0, v);
+      bstore(wlds0, i, v);
+    }
+  }
   if (tid < WN * 32) {
     const int j = nt0 * 32 + tid;
     sbias[tid] = j < a.cout ? a.bias[j] : 0.f;
   }
 
-  const int pix0 = (((wave * WM) * a.sin) * a.ic + li) * PSH;  // strip m adds m * pix_m
-  const int pix_m = a.sin * a.ic * PSH;
+  const int pix0 = (((wave * WM) * a.sin) * a.ic + li) * 8;  // strip m adds m * pix_m (halves)
+  const int pix_m = a.sin * a.ic * 8;
   // tap window offsets live one per lane; v_readlane turns them into wave-uniform scalars
   // without a memory wait inside the k-loop
   const int tap_tab = a.toff[cls][lane <= kMaxTapsX ? lane : kMaxTapsX];
@@ -238,6 +267,8 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(const X3Args a) {
       const int s_ch = last ? 0 : ch + 1;
       const bool stage_next = (DBG & 1) ? false : s_tile < t_end;
       const uint4* wch = wcls + (size_t)ch * nq * a.ntp * kFrag;
+      const _Float16* wcur = wlds0 + buf * (a.bq * 8);
+      _Float16* wnxt = wlds0 + (buf ^ 1) * (a.bq * 8);
       // k-step q: lane half lh takes k8-block kb = 2q + lh = (tap kb / C8, octet kb % C8)
       auto load = [&](int q, Ops& op) {
         int toff;
@@ -246,7 +277,7 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(const X3Args a) {
           const int t1 = __builtin_amdgcn_readlane(tap_tab, 2 * q + 1);
           toff = lh ? t1 : t0;
         } else {
-          toff = __builtin_amdgcn_readlane(tap_tab, (2 * q) / C8) + (((2 * q) & (C8 - 1)) + lh) * 8;
+          toff = __builtin_amdgcn_readlane(tap_tab, (2 * q) / C8) + (((2 * q) & (C8 - 1)) + lh) * a.ps;
         }
 #pragma unroll
         for (int m = 0; m < WM; ++m) {
@@ -255,13 +286,17 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(const X3Args a) {
             op.al[m] = op.ah[m];
           } else {
             op.ah[m] = *reinterpret_cast<const h8*>(cur + pix0 + m * pix_m + toff);
-            op.al[m] = *reinterpret_cast<const h8*>(cur + pix0 + m * pix_m + toff + CC);
+            op.al[m] = *reinterpret_cast<const h8*>(cur + pix0 + m * pix_m + toff + C8 * a.ps);
           }
         }
         const uint4* wk = wch + ((size_t)q * a.ntp + nt0) * kFrag + lane;
+        const uint4* wl = reinterpret_cast<const uint4*>(wcur) + q * (WN * kFrag) + lane;
 #pragma unroll
         for (int n = 0; n < WN; ++n) {
-          if constexpr (DBG & 2) {
+          if constexpr (BL != 0) {
+            op.bh[n] = wl[n * kFrag];
+            op.bl[n] = wl[n * kFrag + 64];
+          } else if constexpr (DBG & 2) {
             op.bh[n] = make_uint4(q, n, 1, 2);
             op.bl[n] = op.bh[n];
             if constexpr (kSingleAcc) op.bd[n] = op.bh[n];
@@ -310,7 +345,57 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(const X3Args a) {
         store(nxt, st);
       };
       int staged = 0;
-      if constexpr (kSingleAcc) {
+      if constexpr (BL != 0) {
+        // weights from LDS: the k-loop's only global loads are the staging fetches. One A item
+        // (first half) and one weight item (second half) per staged pair, unconditionally (items
+        // past either count load a clamped index and skip the LDS write: branching between
+        // staged and plain halves instead costs ~80 VGPRs and spills at WM = WN = 2).
+        Ops S0, S1;
+        load(0, S0);
+        const int nA = stage_next ? nstage : 0;
+        const int nB = stage_next ? nbstage : 0;
+        const int npair = nq >> 1;
+        const int nst = min(max(nA, nB), npair);
+        const int spread = nst ? max(1, npair / nst) : 1;
+        int q = 0;
+        // every staged load gets more than one half-step of MFMAs to land behind: the A item
+        // fetched in the first half is written after the second half's MFMAs, the weight item
+        // fetched in the second half after the next staged pair's first half
+        uint4 vb;
+        for (; staged < nst; ++staged) {
+          load(q + 1 < nq ? q + 1 : nq - 1, S1);
+          Stage st;
+          fetch(tid + staged * NT, s_tile, s_ch, st);
+          __builtin_amdgcn_sched_barrier(0);
+          mfmas(S0);
+          __builtin_amdgcn_sched_barrier(0);
+          if (staged > 0) bstore(wnxt, tid + (staged - 1) * NT, vb);
+          load(q + 2 < nq ? q + 2 : nq - 1, S0);
+          uint4 vn;
+          bfetch(tid + staged * NT, s_ch, vn);
+          __builtin_amdgcn_sched_barrier(0);
+          mfmas(S1);
+          __builtin_amdgcn_sched_barrier(0);
+          store(nxt, st);
+          vb = vn;
+          q += 2;
+          for (int r = 1; r < spread; ++r, q += 2) {
+            half_plain(q, S0, S1);
+            half_plain(q + 1, S1, S0);
+          }
+        }
+        for (; q + 1 < nq; q += 2) {
+          half_plain(q, S0, S1);
+          half_plain(q + 1, S1, S0);
+        }
+        if (nq & 1) mfmas(S0);
+        if (nst > 0) bstore(wnxt, tid + (nst - 1) * NT, vb);
+        for (int qs = staged; qs < nB; ++qs) {
+          uint4 v;
+          bfetch(tid + qs * NT, s_ch, v);
+          bstore(wnxt, tid + qs * NT, v);
+        }
+      } else if constexpr (kSingleAcc) {
         // prefetch distance 2 (the single accumulator leaves room for three operand sets): step
         // q multiplies S[q % 3] and loads k-step q+2 into the set step q-1 just finished with
         auto step_plain = [&](int q, const Ops& use, Ops& nxt_ops) {
@@ -394,46 +479,75 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(const X3Args a) {
     // channels N-tile*32 + 8g + 4lh + {0..3} -> one 16-B store (and residual load) per group.
     // Activation as one max: relu = max(v, 0*v), lrelu = max(v, 0.1*v), none = max(v, 1*v).
     const int qy0 = (tile / tiles_x) * TH, qx0 = (tile % tiles_x) * TW;
+    // y and res through buffer descriptors with 32-bit offsets (the host keeps each launch's
+    // output under 4 GB): one offset register per output tile instead of 64-bit addresses, and a
+    // store whose lane is outside the output (past Wq / Hq / coutp) gets an offset past the
+    // descriptor's range, which the hardware drops -- no branches. Residual loads of such lanes
+    // read 0 or unused values.
+    const __amdgpu_buffer_rsrc_t ry =
+        __builtin_amdgcn_make_buffer_rsrc((void*)a.y, (short)0, (int)a.y_bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rr =
+        __builtin_amdgcn_make_buffer_rsrc((void*)a.res, (short)0, (int)a.y_bytes, 0x00020000);
+    constexpr unsigned kOob = 0xFFFFFF00u;
     const bool px_ok = qx0 + li < a.Wq;
+    auto voff_of = [&](int m, int n) {
+      const unsigned qy = qy0 + wave * WM + m;
+      return (((unsigned)b * a.Ho + qy * a.sout + a.oy0[cls]) * a.Wo + a.ox0[cls] +
+              (unsigned)(qx0 + li) * a.sout) * (unsigned)a.coutp * 4u + (unsigned)((nt0 + n) * 32 + 4 * lh) * 4u;
+    };
+    // residual: the 4 groups of output tile t+1 are loaded before tile t is finished and stored,
+    // so each wait covers loads issued one tile earlier (vmcnt is in order and counts the stores);
+    // WM = WN = 2 has no registers for the second set: its 4 loads are waited for together
+    constexpr int NTL = WM * WN;
+    constexpr bool kResPipe = NTL < 4;
+    float4 rv[2][4];
+    auto load_res = [&](int t, float4 (&r)[4]) {
+      const unsigned vo = voff_of(t / WN, t % WN);
 #pragma unroll
-    for (int n = 0; n < WN; ++n) {
+      for (int g = 0; g < 4; ++g)
+        r[g] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rr, vo + 32u * g, 0, 0));
+    };
+    if (a.res && kResPipe) load_res(0, rv[0]);
 #pragma unroll
-      for (int m = 0; m < WM; ++m) {
-        const int qy = qy0 + wave * WM + m;
-        if (qy >= a.Hq || (nt0 + n) * 32 >= a.coutp) continue;  // wave-uniform
-        const size_t prow = (((size_t)b * a.Ho + qy * a.sout + a.oy0[cls]) * a.Wo + a.ox0[cls] +
-                             (size_t)(qx0 + li) * a.sout) * a.coutp;
+    for (int t = 0; t < NTL; ++t) {
+      const int m = t / WN, n = t % WN;
+      if (a.res) {
+        if (!kResPipe) load_res(t, rv[t & 1]);
+        else if (t + 1 < NTL) load_res(t + 1, rv[(t + 1) & 1]);
+      }
+      const unsigned vo = voff_of(m, n);
+      const bool row_ok = qy0 + wave * WM + m < a.Hq && px_ok;
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int jl = 8 * g + 4 * lh;       // channel within the N-tile
-          const int j0 = (nt0 + n) * 32 + jl;  // first of this lane's 4 channels
-          if (j0 >= a.coutp) continue;         // cout <= 4 layers: only g = 0, lh = 0
-          const float4 bj = *reinterpret_cast<const float4*>(sbias + n * 32 + jl);
-          const float bb[4] = {bj.x, bj.y, bj.z, bj.w};
-          float v[4];
+      for (int g = 0; g < 4; ++g) {
+        const int jl = 8 * g + 4 * lh;       // channel within the N-tile
+        const int j0 = (nt0 + n) * 32 + jl;  // first of this lane's 4 channels
+        const float4 bj = *reinterpret_cast<const float4*>(sbias + n * 32 + jl);
+        const float bb[4] = {bj.x, bj.y, bj.z, bj.w};
+        float v[4];
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int r = 4 * g + i;
-            float t;
-            if constexpr (kSingleAcc) t = acc[m][n][r] * a.osc + bb[i];
-            else t = fmaf(cor[m][n][r], a.osc_c, acc[m][n][r] * a.osc) + bb[i];
-            v[i] = fmaxf(t, t * a.act_slope);
-          }
-          if (a.res && px_ok) {
-            const float4 rv = *reinterpret_cast<const float4*>(a.res + prow + j0);
-            v[0] += rv.x; v[1] += rv.y; v[2] += rv.z; v[3] += rv.w;
-          }
-          if (a.post_op == FVC_POST_EXP) {
+        for (int i = 0; i < 4; ++i) {
+          const int r = 4 * g + i;
+          float tv;
+          if constexpr (kSingleAcc) tv = acc[m][n][r] * a.osc + bb[i];
+          else tv = fmaf(cor[m][n][r], a.osc_c, acc[m][n][r] * a.osc) + bb[i];
+          v[i] = fmaxf(tv, tv * a.act_slope);
+        }
+        if (a.res) {
+          const float4 q4 = rv[t & 1][g];
+          v[0] += q4.x; v[1] += q4.y; v[2] += q4.z; v[3] += q4.w;
+        }
+        if (a.post_op == FVC_POST_EXP) {
 #pragma unroll
-            for (int i = 0; i < 4; ++i) v[i] = expf(v[i]);
-          }
+          for (int i = 0; i < 4; ++i) v[i] = expf(v[i]);
+        }
 #pragma unroll
-          for (int i = 0; i < 4; ++i) v[i] = j0 + i < a.cout ? v[i] : 0.f;  // pad channels = 0
-          if constexpr (DBG & 4) {
-            asm volatile("" ::"v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]));
-          } else {
-            if (px_ok) *reinterpret_cast<float4*>(a.y + prow + j0) = make_float4(v[0], v[1], v[2], v[3]);
-          }
+        for (int i = 0; i < 4; ++i) v[i] = j0 + i < a.cout ? v[i] : 0.f;  // pad channels = 0
+        const unsigned so = (row_ok && j0 < a.coutp) ? vo + 32u * g : kOob;
+        if constexpr (DBG & 4) {
+          asm volatile("" ::"v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]), "v"(so));
+        } else {
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, make_float4(v[0], v[1], v[2], v[3])),
+                                                 ry, so, 0, 0);
         }
       }
     }
@@ -453,6 +567,13 @@ struct X3Cfg {
 };
 
 static int x3_floordiv(int a, int b) { return (a >= 0) ? a / b : -((-a + b - 1) / b); }
+
+// LDS A tile: 2*CC/8 planes (hi octets, then lo octets) of ir*ic 16-B pixel entries. The plane
+// stride is the pixel count rounded up to 4 mod 16 entries (64 B mod 256 B), so the staging
+// writes of consecutive items (octets of one pixel go to different planes) do not collide, while
+// a strip read (32 consecutive pixels of one plane, 16 B each) is conflict-free by construction.
+static int x3_plane_pix(int ir, int ic) { return ((ir * ic + 15) & ~15) + 4; }
+static size_t x3_tile_bytes(int ir, int ic, int cc) { return (size_t)4 * cc * x3_plane_pix(ir, ic); }
 
 static int env_int(const char* n, int dflt) {
   const char* v = getenv(n);
@@ -533,7 +654,7 @@ static bool x3_cfg(int cin, int cout, int ks, int stride, int transposed, X3Cfg&
     c.th = c.nw * c.wm;
     const int ir = (c.th - 1) * c.sin + 1 + (c.dymax - c.dymin);
     const int ic = 31 * c.sin + 1 + (c.dxmax - c.dxmin);
-    const size_t lds = 256 + 2 * ((((size_t)ir * ic * (2 * c.cc + 8)) + 7) & ~(size_t)7) * 2;
+    const size_t lds = 256 + 2 * x3_tile_bytes(ir, ic, c.cc);
     if (lds <= 160 * 1024) break;
     if (c.cc > 8 && c.cinp % (c.cc / 2) == 0) c.cc /= 2;
     else if (c.wm > 1) c.wm /= 2;
@@ -572,12 +693,12 @@ static int x3_kw(const float* w, size_t n) {
   return kw < -100 ? -100 : (kw > 100 ? 100 : kw);
 }
 
-template <int CC, int WM, int WN, int IOP, int DBG>
+template <int CC, int WM, int WN, int IOP, int BL, int DBG>
 static int x3_launch_d(const X3Args& a, dim3 grid, size_t lds, hipStream_t s) {
   if (lds > 64 * 1024)
-    (void)hipFuncSetAttribute((const void*)conv_x3_kernel<CC, WM, WN, 8, IOP, DBG>,
+    (void)hipFuncSetAttribute((const void*)conv_x3_kernel<CC, WM, WN, 8, IOP, BL, DBG>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL((conv_x3_kernel<CC, WM, WN, 8, IOP, DBG>), grid, dim3(8 * 64), lds, s, a);
+  hipLaunchKernelGGL((conv_x3_kernel<CC, WM, WN, 8, IOP, BL, DBG>), grid, dim3(8 * 64), lds, s, a);
   FVC_CHECK_LAUNCH();
   return 0;
 }
@@ -590,43 +711,53 @@ static int x3_dbg() {
 }
 #endif
 
-template <int CC, int WM, int WN, int IOP>
+template <int CC, int WM, int WN, int IOP, int BL>
 static int x3_launch_t(const X3Args& a, dim3 grid, size_t lds, hipStream_t s) {
 #ifdef FVC_X3_ABLATE
   if (CC == 16 && WM == 2 && WN == 2 && IOP == 0) {
     switch (x3_dbg()) {
-      case 1: return x3_launch_d<CC, WM, WN, IOP, 1>(a, grid, lds, s);
-      case 2: return x3_launch_d<CC, WM, WN, IOP, 2>(a, grid, lds, s);
-      case 4: return x3_launch_d<CC, WM, WN, IOP, 4>(a, grid, lds, s);
-      case 8: return x3_launch_d<CC, WM, WN, IOP, 8>(a, grid, lds, s);
-      case 3: return x3_launch_d<CC, WM, WN, IOP, 3>(a, grid, lds, s);
-      case 15: return x3_launch_d<CC, WM, WN, IOP, 15>(a, grid, lds, s);
-      case 11: return x3_launch_d<CC, WM, WN, IOP, 11>(a, grid, lds, s);
+      case 1: return x3_launch_d<CC, WM, WN, IOP, BL, 1>(a, grid, lds, s);
+      case 2: return x3_launch_d<CC, WM, WN, IOP, BL, 2>(a, grid, lds, s);
+      case 4: return x3_launch_d<CC, WM, WN, IOP, BL, 4>(a, grid, lds, s);
+      case 8: return x3_launch_d<CC, WM, WN, IOP, BL, 8>(a, grid, lds, s);
+      case 3: return x3_launch_d<CC, WM, WN, IOP, BL, 3>(a, grid, lds, s);
+      case 15: return x3_launch_d<CC, WM, WN, IOP, BL, 15>(a, grid, lds, s);
+      case 11: return x3_launch_d<CC, WM, WN, IOP, BL, 11>(a, grid, lds, s);
       default: break;
     }
   }
 #endif
-  return x3_launch_d<CC, WM, WN, IOP, 0>(a, grid, lds, s);
+  return x3_launch_d<CC, WM, WN, IOP, BL, 0>(a, grid, lds, s);
 }
 
-template <int CC, int WM, int WN>
+template <int CC, int WM, int WN, int BL>
 static int x3_launch_iop(int iop, const X3Args& a, dim3 grid, size_t lds, hipStream_t s) {
   switch (iop) {
-    case FVC_IN_NONE: return x3_launch_t<CC, WM, WN, FVC_IN_NONE>(a, grid, lds, s);
-    case FVC_IN_RELU: return x3_launch_t<CC, WM, WN, FVC_IN_RELU>(a, grid, lds, s);
-    case FVC_IN_ABS: return x3_launch_t<CC, WM, WN, FVC_IN_ABS>(a, grid, lds, s);
-    case FVC_IN_ROUND: return x3_launch_t<CC, WM, WN, FVC_IN_ROUND>(a, grid, lds, s);
+    case FVC_IN_NONE: return x3_launch_t<CC, WM, WN, FVC_IN_NONE, BL>(a, grid, lds, s);
+    case FVC_IN_RELU: return x3_launch_t<CC, WM, WN, FVC_IN_RELU, BL>(a, grid, lds, s);
+    case FVC_IN_ABS: return x3_launch_t<CC, WM, WN, FVC_IN_ABS, BL>(a, grid, lds, s);
+    case FVC_IN_ROUND: return x3_launch_t<CC, WM, WN, FVC_IN_ROUND, BL>(a, grid, lds, s);
   }
   return FVC_EINVAL;
 }
 
-// instantiated shapes (8 waves, 2 per SIMD, <= 256 registers: scripts/kres.sh): WM, WN in {1, 2}
+template <int CC, int WM, int WN>
+static int x3_launch_bl(int bl, int iop, const X3Args& a, dim3 grid, size_t lds, hipStream_t s) {
+  if constexpr (!kSingleAcc) {
+    if (bl) return x3_launch_iop<CC, WM, WN, 1>(iop, a, grid, lds, s);
+  }
+  return x3_launch_iop<CC, WM, WN, 0>(iop, a, grid, lds, s);
+}
+
+// instantiated shapes (8 waves, 2 per SIMD, <= 256 registers: scripts/kres.sh): WM, WN in {1, 2},
+// weights from L2 (BL=0) or staged per chunk in LDS (BL=1)
 template <int CC>
-static int x3_launch_cc(int wm, int wn, int iop, const X3Args& a, dim3 grid, size_t lds, hipStream_t s) {
-  if (wm == 2 && wn == 2) return x3_launch_iop<CC, 2, 2>(iop, a, grid, lds, s);
-  if (wm == 2 && wn == 1) return x3_launch_iop<CC, 2, 1>(iop, a, grid, lds, s);
-  if (wm == 1 && wn == 2) return x3_launch_iop<CC, 1, 2>(iop, a, grid, lds, s);
-  if (wm == 1 && wn == 1) return x3_launch_iop<CC, 1, 1>(iop, a, grid, lds, s);
+static int x3_launch_cc(int wm, int wn, int bl, int iop, const X3Args& a, dim3 grid, size_t lds,
+                        hipStream_t s) {
+  if (wm == 2 && wn == 2) return x3_launch_bl<CC, 2, 2>(bl, iop, a, grid, lds, s);
+  if (wm == 2 && wn == 1) return x3_launch_bl<CC, 2, 1>(bl, iop, a, grid, lds, s);
+  if (wm == 1 && wn == 2) return x3_launch_bl<CC, 1, 2>(bl, iop, a, grid, lds, s);
+  if (wm == 1 && wn == 1) return x3_launch_bl<CC, 1, 1>(bl, iop, a, grid, lds, s);
   return FVC_EINVAL;
 }
 
@@ -648,6 +779,20 @@ static int run_x3(const float* x, const void* wpack, float osc, const float* bia
     a.Ho = h * stride; a.Wo = w * stride;
     a.Hq = h; a.Wq = w;
   }
+  // y and res are addressed through buffer descriptors with 32-bit offsets: split batches whose
+  // output tensor reaches 4 GB into launches over sub-batches
+  const unsigned long long ybytes = (unsigned long long)batch * a.Ho * a.Wo * a.coutp * 4ull;
+  if (ybytes >= (1ull << 32) - 4096) {
+    if (batch == 1) return FVC_EINVAL;
+    const int b1 = batch / 2;
+    const size_t xs = (size_t)h * w * c.cinp, ys = (size_t)a.Ho * a.Wo * a.coutp;
+    int rc = run_x3(x, wpack, osc, bias, res, y, b1, h, w, cin, cout, ks, stride, transposed, in_op, act,
+                    post_op, s);
+    if (rc) return rc;
+    return run_x3(x + b1 * xs, wpack, osc, bias, res + b1 * ys, y + b1 * ys, batch - b1, h, w, cin, cout, ks,
+                  stride, transposed, in_op, act, post_op, s);
+  }
+  a.y_bytes = (unsigned)ybytes;
   a.sin = c.sin; a.sout = c.sout; a.nclass = c.nclass; a.nchunks = c.nchunks; a.ntp = c.ntp;
   a.dymin = c.dymin; a.dxmin = c.dxmin;
   a.ir = (c.th - 1) * c.sin + 1 + (c.dymax - c.dymin);
@@ -666,7 +811,7 @@ static int run_x3(const float* x, const void* wpack, float osc, const float* bia
     a.ox0[cl] = v ? c.ox0[cl] : 0;
     a.wcls[cl] = v ? c.wcls[cl] : 0;
   }
-  const int psh = 2 * c.cc + 8;
+  a.ps = x3_plane_pix(a.ir, a.ic) * 8;
   for (int cl = 0; cl < 4; ++cl)
     for (int t = 0; t <= kMaxTapsX; ++t) {
       int off = 0;
@@ -674,12 +819,11 @@ static int run_x3(const float* x, const void* wpack, float osc, const float* bia
         const int cdy = c.tdy[cl][t] - c.dymin;
         const int cdx = c.tdx[cl][t] - c.dxmin;
         const int cpos = a.half ? ((cdx & 1) * a.half + (cdx >> 1)) : cdx;
-        off = (cdy * a.ic + cpos) * psh;
+        off = (cdy * a.ic + cpos) * 8;
       }
       a.toff[cl][t] = off;
     }
-  const size_t tile_h = ((size_t)a.ir * a.ic * psh + 7) & ~(size_t)7;
-  const size_t lds = 256 + 2 * tile_h * 2;
+  size_t lds = 256 + 2 * x3_tile_bytes(a.ir, a.ic, c.cc);
   if (lds > 160 * 1024) return FVC_EINVAL;
   const int tiles_x = fvc_cdiv(a.Wq, 32);
   const int tiles_y = fvc_cdiv(a.Hq, c.th);
@@ -701,10 +845,20 @@ static int run_x3(const float* x, const void* wpack, float osc, const float* bia
   if (gx > (long long)tiles_x * tiles_y) gx = (long long)tiles_x * tiles_y;
   if (gx < 1) gx = 1;
   dim3 grid((unsigned)gx, c.ntp / wn, batch * c.nclass);
+  // weights: staged per channel chunk into two LDS buffers (one copy per block instead of one
+  // L2 stream per wave) when both fit next to the A buffers; else read from L2 by every wave.
+  // FVC_X3_BLDS=0 forces L2.
+  int nks_max = 0;
+  for (int cl = 0; cl < c.nclass; ++cl) nks_max = c.nks[cl] > nks_max ? c.nks[cl] : nks_max;
+  a.bq = nks_max * wn * kFrag;
+  const size_t lds_bl = lds + 2 * (size_t)a.bq * 16;
+  const int bl = (!kSingleAcc && env_int("FVC_X3_BLDS", 1) != 0 && lds_bl <= 160 * 1024) ? 1 : 0;
+  if (bl) lds = lds_bl;
+  else a.bq = 0;
   switch (c.cc) {
-    case 8: return x3_launch_cc<8>(c.wm, wn, in_op, a, grid, lds, s);
-    case 16: return x3_launch_cc<16>(c.wm, wn, in_op, a, grid, lds, s);
-    case 32: return x3_launch_cc<32>(c.wm, wn, in_op, a, grid, lds, s);
+    case 8: return x3_launch_cc<8>(c.wm, wn, bl, in_op, a, grid, lds, s);
+    case 16: return x3_launch_cc<16>(c.wm, wn, bl, in_op, a, grid, lds, s);
+    case 32: return x3_launch_cc<32>(c.wm, wn, bl, in_op, a, grid, lds, s);
   }
   return FVC_EINVAL;
 }

@@ -28,6 +28,9 @@ CASES = {
     "c3_64_3_full": (64, 3, 3, 1, False, 1088, 1920),
     "d5_64_3_half": (64, 3, 5, 2, True, 1088, 1920),
     "c7_16_2_full": (16, 2, 7, 1, False, 1088, 1920),
+    # Warp_net ResBlock second conv: relu on the input, residual add in the epilogue
+    "c3_64_full_res": (64, 64, 3, 1, False, 1088, 1920, "res"),
+    "c3_64_half_res": (64, 64, 3, 1, False, 544, 960, "res"),
 }
 
 ap = argparse.ArgumentParser()
@@ -36,18 +39,22 @@ ap.add_argument("--iters", type=int, default=10)
 args = ap.parse_args()
 dev = torch.device("cuda")
 for name in args.cases.split(","):
-    cin, cout, k, s, tr, H, W = CASES[name]
+    cin, cout, k, s, tr, H, W = CASES[name][:7]
+    with_res = len(CASES[name]) > 7
     if tr:
         H, W = H // 2, W // 2
     w = torch.randn((cin, cout, k, k) if tr else (cout, cin, k, k)) * 0.05
     pc = K.PackedConv(w, torch.zeros(cout), k, s, tr, dev)
     x = torch.randn(1, H, W, K.cp4(cin), device=dev)
-    y = pc(x)
+    kw = {}
+    if with_res:
+        kw = dict(in_op=K.IN_RELU, res=torch.randn(1, H, W, K.cp4(cout), device=dev))
+    y = pc(x, **kw)
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(args.iters):
-        pc(x, out=y)
+        pc(x, out=y, **kw)
     e1.record()
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / args.iters

@@ -97,6 +97,28 @@ def test_conv(dev, case, precision):
         assert float(yc[..., cout:].abs().max()) == 0.0, "pad channels must be zero"
 
 
+@pytest.mark.parametrize("case", [CONV_CASES[i] for i in (0, 8, 11, 12, 19)],
+                         ids=lambda c: f"ci{c[0]}co{c[1]}k{c[2]}s{c[3]}{'T' if c[4] else ''}")
+def test_conv_x3_weight_paths_identical(dev, case, monkeypatch):
+    """Weights staged per chunk in LDS (default where they fit) and weights read from L2 by every
+    wave (FVC_X3_BLDS=0) feed the same MFMAs in the same order: bit-identical outputs."""
+    cin, cout, k, s, tr, H, W, in_op, act, post, with_res = case
+    g = torch.Generator().manual_seed(7 + cin + cout)
+    x = to_nhwc(torch.randn(2, cin, H, W, generator=g)).to(dev)
+    w = torch.randn((cin, cout, k, k) if tr else (cout, cin, k, k), generator=g) * (1.0 / (cin * k * k) ** 0.5)
+    b = torch.randn(cout, generator=g) * 0.1
+    pc = K.PackedConv(w, b, k, s, tr, dev, precision="x3")
+    assert pc.x3
+    ho, wo = pc.out_hw(H, W)
+    res = to_nhwc(torch.randn(2, cout, ho, wo, generator=g)).to(dev) if with_res else None
+    outs = []
+    for bl in ("1", "0"):
+        monkeypatch.setenv("FVC_X3_BLDS", bl)
+        outs.append(pc(x, in_op=in_op, act=act, post=post, res=res))
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+
+
 def test_conv_x3_overflow_flag(dev):
     """|activation| >= 65000 cannot be split into fp16 halves: the x3 kernel must flag it."""
     w = torch.randn(64, 64, 3, 3) * 0.05
