@@ -58,6 +58,13 @@ constexpr bool kSingleAcc = true;
 #else
 constexpr bool kSingleAcc = false;
 #endif
+// Staged items split between the MFMA tiles of the next half-step (-DFVC_X3_ILV, experiment):
+// measured neutral to 2 % slower than splitting after the MFMAs (scripts/conv_micro.py), so off.
+#ifdef FVC_X3_ILV
+constexpr bool kInterleave = true;
+#else
+constexpr bool kInterleave = false;
+#endif
 constexpr int kNPL = kSingleAcc ? 3 : 2;   // weight planes per (k-step, N-tile)
 constexpr int kFrag = 64 * kNPL;          // uint4 per (k-step, N-tile)
 
@@ -130,9 +137,10 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(const X3Args a) {
 
   extern __shared__ __attribute__((aligned(16))) _Float16 smh[];
   const int tile_h = 2 * C8 * a.ps;  // halves per A buffer: 2*C8 planes (hi octets, lo octets)
-  _Float16* const tile0 = smh + 128;  // two buffers at tile0 and tile0 + tile_h (LDS pointers;
+  _Float16* const tile0 = smh + 256;  // two buffers at tile0 and tile0 + tile_h (LDS pointers;
                                       // no pointer array, which would degrade them to flat)
   float* const sbias = reinterpret_cast<float*>(smh);  // [WN * 32] bias of this block's N-tiles
+  _Float16* const sdump = smh + 128;  // 32 B sink for staging writes of items past the tile
   // BL: two weight buffers after the A buffers, each [k-step][N-tile][hi|lo][lane] uint4
   _Float16* const wlds0 = tile0 + 2 * tile_h;
 
@@ -141,23 +149,27 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(const X3Args a) {
   const int wave = tid >> 6;
   const int li = lane & 31;
   const int lh = lane >> 5;
-  const int cls = blockIdx.z % a.nclass;
-  const int b = blockIdx.z / a.nclass;
+  const int b = blockIdx.z;
   const int tiles_x = (a.Wq + TW - 1) / TW;
   const int ntiles = tiles_x * ((a.Hq + TH - 1) / TH);
-  // persistent over a contiguous run of spatial tiles (row-major: neighbours share halo rows and
-  // columns in this CU's L2); the staging pipeline runs on across tile boundaries
-  const int t_begin = (int)(((long long)ntiles * blockIdx.x) / gridDim.x);
-  const int t_end = (int)(((long long)ntiles * (blockIdx.x + 1)) / gridDim.x);
-  if (t_begin >= t_end) return;
+  // persistent over a contiguous run of work items w = tile * nclass + class (row-major tiles:
+  // neighbours share halo rows and columns in this CU's L2; all parity classes of a transposed
+  // conv's tile run back to back on one CU, so their shared input tile is fetched from HBM once
+  // and every block gets the same mix of 4- / 2- / 1-tap classes); the staging pipeline runs on
+  // across item boundaries
+  const int nitems = ntiles * a.nclass;
+  const int w_begin = (int)(((long long)nitems * blockIdx.x) / gridDim.x);
+  const int w_end = (int)(((long long)nitems * (blockIdx.x + 1)) / gridDim.x);
+  if (w_begin >= w_end) return;
   const int nt0 = blockIdx.y * WN;
-  const int nq = a.nks[cls];
+  int cls = w_begin % a.nclass;
+  int nq = a.nks[cls];
   const int hf = a.half;
   const int nch = a.nchunks;
   const int tile_items = a.ir * a.ic * C8;
   const int nstage = (tile_items + NT - 1) / NT;
   const float* xb = a.x + (size_t)b * a.H * a.W * a.cinp;
-  const uint4* wcls = a.w + a.wcls[cls];
+  const uint4* wcls = a.w + a.wcls[cls];  // (cls, nq, wcls, tap_tab: updated per work item)
   float mx = 0.f;  // max |staged value| (fp16 representability check)
 
   // one staging item = 8 channels of one halo pixel: 2 x float4 global -> hi/lo h8 in LDS.
@@ -193,10 +205,12 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(const X3Args a) {
     for (int i = 0; i < 8; ++i) v[i] = st.inb ? in_op_t<IOP>(v[i]) : 0.f;
     h8 hi, lo;
     split8(v, hi, lo, mx);
-    if (st.ok) {
-      *reinterpret_cast<h8*>(t + st.dst) = hi;
-      *reinterpret_cast<h8*>(t + st.dst + C8 * a.ps) = lo;
-    }
+    // branch-free (keeps the split in the MFMA basic block for interleaving): items past the
+    // tile write to a sink
+    _Float16* const ph = st.ok ? t + st.dst : sdump;
+    _Float16* const pl = st.ok ? t + st.dst + C8 * a.ps : sdump + 8;
+    *reinterpret_cast<h8*>(ph) = hi;
+    *reinterpret_cast<h8*>(pl) = lo;
   };
   // BL: one weight staging item = one uint4 of the next chunk's [k-step][N-tile][hi|lo][lane]
   // block slice (contiguous per k-step: N-tiles nt0..nt0+WN-1 are adjacent in the pack)
@@ -214,7 +228,7 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(const X3Args a) {
 
   for (int e = tid; e < tile_items; e += NT) {
     Stage st;
-    fetch(e, t_begin, 0, st);
+    fetch(e, w_begin / a.nclass, 0, st);
     store(tile0, st);
   }
   if constexpr (BL != 0) {
@@ -233,7 +247,7 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(const X3Args a) {
   const int pix_m = a.sin * a.ic * 8;
   // tap window offsets live one per lane; v_readlane turns them into wave-uniform scalars
   // without a memory wait inside the k-loop
-  const int tap_tab = a.toff[cls][lane <= kMaxTapsX ? lane : kMaxTapsX];
+  int tap_tab = a.toff[cls][lane <= kMaxTapsX ? lane : kMaxTapsX];
   __syncthreads();
 
   struct Ops {
@@ -242,7 +256,14 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(const X3Args a) {
   };
   f32x16 acc[WM][WN], cor[WM][kSingleAcc ? 1 : WN];
   int buf = 0;  // LDS buffer holding the chunk being multiplied
-  for (int tile = t_begin; tile < t_end; ++tile) {
+  for (int w = w_begin; w < w_end; ++w) {
+    const int tile = w / a.nclass;
+    if (w != w_begin) {
+      cls = w % a.nclass;
+      nq = a.nks[cls];
+      wcls = a.w + a.wcls[cls];
+      tap_tab = a.toff[cls][lane <= kMaxTapsX ? lane : kMaxTapsX];
+    }
 #pragma unroll
     for (int m = 0; m < WM; ++m)
 #pragma unroll
@@ -263,9 +284,10 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(const X3Args a) {
       const _Float16* cur = tile0 + buf * tile_h;
       _Float16* nxt = tile0 + (buf ^ 1) * tile_h;
       const bool last = ch + 1 == nch;
-      const int s_tile = last ? tile + 1 : tile;
+      const int s_item = last ? w + 1 : w;
+      const int s_tile = s_item / a.nclass;
       const int s_ch = last ? 0 : ch + 1;
-      const bool stage_next = (DBG & 1) ? false : s_tile < t_end;
+      const bool stage_next = (DBG & 1) ? false : s_item < w_end;
       const uint4* wch = wcls + (size_t)ch * nq * a.ntp * kFrag;
       const _Float16* wcur = wlds0 + buf * (a.bq * 8);
       _Float16* wnxt = wlds0 + (buf ^ 1) * (a.bq * 8);
@@ -307,11 +329,9 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(const X3Args a) {
           }
         }
       };
-      auto mfmas = [&](const Ops& op) {
-#pragma unroll
-        for (int m = 0; m < WM; ++m)
-#pragma unroll
-          for (int n = 0; n < WN; ++n) {
+      auto mfma_tile = [&](const Ops& op, const int m, const int n) {
+        {
+          {
             const h8 wh = __builtin_bit_cast(h8, op.bh[n]);
             const h8 wl = __builtin_bit_cast(h8, op.bl[n]);
             // weights as the A (row) operand, pixels as B: the 32x32 result is channel x pixel,
@@ -328,6 +348,46 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(const X3Args a) {
               cor[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wh, op.al[m], cor[m][n], 0, 0, 0);
             }
           }
+        }
+      };
+      auto mfmas = [&](const Ops& op) {
+#pragma unroll
+        for (int m = 0; m < WM; ++m)
+#pragma unroll
+          for (int n = 0; n < WN; ++n) mfma_tile(op, m, n);
+      };
+      // the MFMAs of one half-step with a staged item's split + LDS write cut into WM*WN slices,
+      // one after each (m, n) tile's three MFMAs; sched_barrier keeps every slice in place, so a
+      // wave converts while its own matrix ops run
+      auto mfmas_split = [&](const Ops& op, const Stage& st) {
+        constexpr int NP = WM * WN;
+        constexpr int PER = 8 / NP;
+        float v[8] = {st.v0.x, st.v0.y, st.v0.z, st.v0.w, st.v1.x, st.v1.y, st.v1.z, st.v1.w};
+        h8 hi, lo;
+#pragma unroll
+        for (int t = 0; t < NP; ++t) {
+          mfma_tile(op, t / WN, t % WN);
+#pragma unroll
+          for (int i = t * PER; i < (t + 1) * PER; i += 2) {
+            const float x0 = st.inb ? in_op_t<IOP>(v[i]) : 0.f;
+            const float x1 = st.inb ? in_op_t<IOP>(v[i + 1]) : 0.f;
+            const f2v x = {x0, x1};
+            const h2v h = __builtin_convertvector(x, h2v);
+            const f2v back = __builtin_convertvector(h, f2v);
+            const h2v l = __builtin_convertvector((x - back) * 2048.f, h2v);
+            // pin the conversion to this slice (pure arithmetic is otherwise free to sink to the
+            // LDS write in instruction selection, where sched_barrier has no say)
+            asm volatile("" ::"v"(h), "v"(l));
+            hi[i] = h[0]; hi[i + 1] = h[1];
+            lo[i] = l[0]; lo[i + 1] = l[1];
+            mx = fmaxf(mx, fmaxf(fabsf(x0), fabsf(x1)));
+          }
+          if (t + 1 < NP) __builtin_amdgcn_sched_barrier(0);
+        }
+        _Float16* const ph = st.ok ? nxt + st.dst : sdump;
+        _Float16* const pl = st.ok ? nxt + st.dst + C8 * a.ps : sdump + 8;
+        *reinterpret_cast<h8*>(ph) = hi;
+        *reinterpret_cast<h8*>(pl) = lo;
       };
       auto half_plain = [&](int q, const Ops& use, Ops& nxt_ops) {
         load(q + 1 < nq ? q + 1 : nq - 1, nxt_ops);
@@ -448,13 +508,39 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(const X3Args a) {
         const int nst = stage_next ? min(nstage, npair) : 0;
         const int spread = nst ? max(1, npair / nst) : 1;
         int q = 0;
-        for (; staged < nst; ++staged) {
-          half_stage(tid + staged * NT, q, S0, S1);
-          half_plain(q + 1, S1, S0);
-          q += 2;
-          for (int r = 1; r < spread; ++r, q += 2) {
-            half_plain(q, S0, S1);
+        if constexpr (kInterleave) {
+          // item i is fetched in staged pair i and split + written in pair i+1, its VALU work
+          // spread between that half-step's MFMAs (sched_group_barrier), so a wave converts while
+          // its own matrix ops run instead of after them
+          Stage sp;  // fetched in the previous staged pair; none before the first (ok = false)
+          sp.v0 = sp.v1 = make_float4(0.f, 0.f, 0.f, 0.f);
+          sp.dst = 0;
+          sp.inb = sp.ok = false;
+          for (; staged < nst; ++staged) {
+            Stage sn;
+            load(q + 1 < nq ? q + 1 : nq - 1, S1);
+            fetch(tid + staged * NT, s_tile, s_ch, sn);
+            __builtin_amdgcn_sched_barrier(0);
+            mfmas_split(S0, sp);
+            __builtin_amdgcn_sched_barrier(0);
+            sp = sn;
             half_plain(q + 1, S1, S0);
+            q += 2;
+            for (int r = 1; r < spread; ++r, q += 2) {
+              half_plain(q, S0, S1);
+              half_plain(q + 1, S1, S0);
+            }
+          }
+          store(nxt, sp);
+        } else {
+          for (; staged < nst; ++staged) {
+            half_stage(tid + staged * NT, q, S0, S1);
+            half_plain(q + 1, S1, S0);
+            q += 2;
+            for (int r = 1; r < spread; ++r, q += 2) {
+              half_plain(q, S0, S1);
+              half_plain(q + 1, S1, S0);
+            }
           }
         }
         for (; q + 1 < nq; q += 2) {
@@ -648,13 +734,15 @@ static bool x3_cfg(int cin, int cout, int ks, int stride, int transposed, X3Cfg&
   // block shape: 8 waves x 2 strips (16 output rows x 32 columns), 2 waves per SIMD;
   // FVC_X3_NW / FVC_X3_WM override for experiments (WM=4 only with 4 waves)
   c.nw = 8;
-  c.wm = env_int("FVC_X3_WM", 2) == 1 ? 1 : 2;
+  // stride-2 convs: one strip per wave (measured 0.22 vs 0.35 ms on the 544x960 128-channel layer:
+  // two strips double the halo rows each staged chunk carries)
+  c.wm = env_int("FVC_X3_WM", (!transposed && stride == 2) ? 1 : 2) == 1 ? 1 : 2;
   // shrink the channel chunk, then the strips per wave, until two tile buffers fit in LDS
   for (;;) {
     c.th = c.nw * c.wm;
     const int ir = (c.th - 1) * c.sin + 1 + (c.dymax - c.dymin);
     const int ic = 31 * c.sin + 1 + (c.dxmax - c.dxmin);
-    const size_t lds = 256 + 2 * x3_tile_bytes(ir, ic, c.cc);
+    const size_t lds = 512 + 2 * x3_tile_bytes(ir, ic, c.cc);
     if (lds <= 160 * 1024) break;
     if (c.cc > 8 && c.cinp % (c.cc / 2) == 0) c.cc /= 2;
     else if (c.wm > 1) c.wm /= 2;
@@ -823,7 +911,7 @@ static int run_x3(const float* x, const void* wpack, float osc, const float* bia
       }
       a.toff[cl][t] = off;
     }
-  size_t lds = 256 + 2 * x3_tile_bytes(a.ir, a.ic, c.cc);
+  size_t lds = 512 + 2 * x3_tile_bytes(a.ir, a.ic, c.cc);
   if (lds > 160 * 1024) return FVC_EINVAL;
   const int tiles_x = fvc_cdiv(a.Wq, 32);
   const int tiles_y = fvc_cdiv(a.Hq, c.th);
@@ -839,20 +927,22 @@ static int run_x3(const float* x, const void* wpack, float osc, const float* bia
   // persistent grid: ~one 8-wave block per CU (FVC_X3_BPC blocks per CU), each walking a
   // contiguous run of spatial tiles
   const int ncu = x3_num_cus();
-  const long long yz = (long long)(c.ntp / wn) * batch * c.nclass;
+  const long long yz = (long long)(c.ntp / wn) * batch;
   const int bpc = env_int("FVC_X3_BPC", 1);
-  long long gx = ((long long)ncu * bpc + yz - 1) / yz;
-  if (gx > (long long)tiles_x * tiles_y) gx = (long long)tiles_x * tiles_y;
+  long long gx = ((long long)ncu * bpc + yz - 1) / yz;  // blocks over all (tile, class) items
+  if (gx > (long long)tiles_x * tiles_y * c.nclass) gx = (long long)tiles_x * tiles_y * c.nclass;
   if (gx < 1) gx = 1;
-  dim3 grid((unsigned)gx, c.ntp / wn, batch * c.nclass);
-  // weights: staged per channel chunk into two LDS buffers (one copy per block instead of one
-  // L2 stream per wave) when both fit next to the A buffers; else read from L2 by every wave.
-  // FVC_X3_BLDS=0 forces L2.
+  dim3 grid((unsigned)gx, c.ntp / wn, batch);
+  // weights: read from L2 by every wave (default), or with FVC_X3_BLDS=1 staged per channel chunk
+  // into two LDS buffers (one copy per block) where both fit next to the A buffers. Measured on
+  // MI355X: the LDS copy is 0-5 % slower -- its ds_reads cost what the L2 reads did -- so it is
+  // kept as an option (tests check both paths give identical bits).
   int nks_max = 0;
   for (int cl = 0; cl < c.nclass; ++cl) nks_max = c.nks[cl] > nks_max ? c.nks[cl] : nks_max;
   a.bq = nks_max * wn * kFrag;
   const size_t lds_bl = lds + 2 * (size_t)a.bq * 16;
-  const int bl = (!kSingleAcc && env_int("FVC_X3_BLDS", 1) != 0 && lds_bl <= 160 * 1024) ? 1 : 0;
+  // (one class per launch only: the weight staging follows the current work item's class)
+  const int bl = (!kSingleAcc && c.nclass == 1 && env_int("FVC_X3_BLDS", 0) != 0 && lds_bl <= 160 * 1024) ? 1 : 0;
   if (bl) lds = lds_bl;
   else a.bq = 0;
   switch (c.cc) {

@@ -100,8 +100,8 @@ def test_conv(dev, case, precision):
 @pytest.mark.parametrize("case", [CONV_CASES[i] for i in (0, 8, 11, 12, 19)],
                          ids=lambda c: f"ci{c[0]}co{c[1]}k{c[2]}s{c[3]}{'T' if c[4] else ''}")
 def test_conv_x3_weight_paths_identical(dev, case, monkeypatch):
-    """Weights staged per chunk in LDS (default where they fit) and weights read from L2 by every
-    wave (FVC_X3_BLDS=0) feed the same MFMAs in the same order: bit-identical outputs."""
+    """Weights staged per chunk in LDS (FVC_X3_BLDS=1, where they fit) and weights read from L2 by
+    every wave (default) feed the same MFMAs in the same order: bit-identical outputs."""
     cin, cout, k, s, tr, H, W, in_op, act, post, with_res = case
     g = torch.Generator().manual_seed(7 + cin + cout)
     x = to_nhwc(torch.randn(2, cin, H, W, generator=g)).to(dev)
