@@ -38,6 +38,8 @@ _SIGS = {
     "fvc_spynet_assemble": (c_int, [vp, vp, vp, vp, vp, c_int, c_int, c_int, vp]),
     "fvc_mc_assemble": (c_int, [vp, vp, vp, vp, c_int, c_int, c_int, vp]),
     "fvc_sub_f32": (c_int, [vp, vp, vp, c_size_t, vp]),
+    "fvc_tap_gather_nhwc": (c_int, [vp, c_int, vp, vp, vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                                    c_int, c_int, vp]),
     "fvc_gdn_nhwc": (c_int, [vp, vp, vp, vp, c_int, c_int, c_int, c_int, c_int, vp]),
     "fvc_reduce_ws_doubles": (c_size_t, []),
     "fvc_recon_finalize": (c_int, [vp] * 7 + [c_int, c_int, c_int, vp]),

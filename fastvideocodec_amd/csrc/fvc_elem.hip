@@ -42,6 +42,58 @@ __global__ void k_nhwc_to_nchw(const float* __restrict__ src, float* __restrict_
 }
 
 // avg_pool2d(k=2,s=2): ((x00 + x01) + x10) + x11, then / 4 (ATen CPU order)
+// Second half of a cout <= 4 conv / transposed conv computed as a tap-partial GEMM (the x3
+// kernel's 1x1 pass writes P[b][iy][ix][t * cout + co] = sum_ci x[b][iy][ix][ci] w_t[ci][co] for
+// every input pixel and tap t = ky * ks + kx): y[b][Y][X][co] = bias[co] + sum over the taps that
+// reach (Y, X) of P at the source pixel, then activation, residual, exp; pad channel 3 (and any
+// co >= cout) = 0. Conv (stride 1): source = (Y + ky - pad, X + kx - pad); transposed (stride s,
+// output padding s - 1): source = ((Y + pad - ky) / s, (X + pad - kx) / s) where divisible.
+// Fixed tap order: deterministic. HBM-bound (P is re-read from L1/L2 by neighbouring outputs).
+template <int KS, int COUT, int TR>
+__global__ __launch_bounds__(256) void k_tap_gather(const float* __restrict__ P, int pcp,
+                                                    const float* __restrict__ bias,
+                                                    const float* __restrict__ res, float* __restrict__ y,
+                                                    int B, int H, int W, int Ho, int Wo, float act_slope,
+                                                    int post_op) {
+  constexpr int pad = KS / 2;
+  const size_t n = (size_t)B * Ho * Wo;
+  for (size_t e = grid_stride_start(); e < n; e += (size_t)gridDim.x * blockDim.x) {
+    const int X = e % Wo;
+    const int Y = (e / Wo) % Ho;
+    const size_t b = e / ((size_t)Wo * Ho);
+    float acc[COUT];
+#pragma unroll
+    for (int co = 0; co < COUT; ++co) acc[co] = bias[co];
+#pragma unroll
+    for (int ky = 0; ky < KS; ++ky) {
+      // transposed (stride 2): only taps with ky = Y + pad (mod 2) reach row Y
+      if (TR && ((Y + pad - ky) & 1)) continue;
+      const int iy = TR ? (Y + pad - ky) >> 1 : Y + ky - pad;  // >> 1: floor for negatives
+      if (iy < 0 || iy >= H) continue;
+#pragma unroll
+      for (int kx = 0; kx < KS; ++kx) {
+        if (TR && ((X + pad - kx) & 1)) continue;
+        const int ix = TR ? (X + pad - kx) >> 1 : X + kx - pad;
+        if (ix < 0 || ix >= W) continue;
+        const float* src = P + ((b * H + iy) * W + ix) * pcp + (ky * KS + kx) * COUT;
+#pragma unroll
+        for (int co = 0; co < COUT; ++co) acc[co] += src[co];
+      }
+    }
+    float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
+    float* ov = &o.x;
+#pragma unroll
+    for (int co = 0; co < COUT; ++co) {
+      float v = acc[co];
+      v = fmaxf(v, v * act_slope);
+      if (res) v += res[e * 4 + co];
+      if (post_op == FVC_POST_EXP) v = expf(v);
+      ov[co] = v;
+    }
+    reinterpret_cast<float4*>(y)[e] = o;
+  }
+}
+
 __global__ void k_avgpool2(const float* __restrict__ src, float* __restrict__ dst, int B, int H, int W,
                            int cp) {
   const int Ho = H / 2, Wo = W / 2, c4n = cp / 4;
@@ -565,6 +617,33 @@ int fvc_mc_assemble(const float* ref, const float* mv, float* warpframe, float* 
                      batch, h, w);
   FVC_CHECK_LAUNCH();
   return 0;
+}
+
+int fvc_tap_gather_nhwc(const float* P, int pcp, const float* bias, const float* res, float* y, int batch,
+                        int h, int w, int cout, int ksize, int stride, int transposed, int act, int post_op,
+                        fvc_stream_t s) {
+  if (!P || !bias || !y || batch <= 0 || h <= 0 || w <= 0 || cout < 1 || cout > 4 ||
+      (ksize != 3 && ksize != 5) || pcp < ksize * ksize * cout || pcp % 4)
+    return FVC_EINVAL;
+  if (transposed ? stride != 2 : stride != 1) return FVC_EINVAL;
+  const int Ho = transposed ? h * stride : h, Wo = transposed ? w * stride : w;
+  const float slope = act == FVC_ACT_RELU ? 0.f : (act == FVC_ACT_LRELU ? 0.1f : 1.f);
+  const size_t n = (size_t)batch * Ho * Wo;
+  const dim3 g(grid_for(n)), bl(kBlk);
+  hipStream_t st = (hipStream_t)s;
+#define FVC_TG(KS, CO, TR)                                                                                   \
+  if (ksize == KS && cout == CO && transposed == TR) {                                                       \
+    hipLaunchKernelGGL((k_tap_gather<KS, CO, TR>), g, bl, 0, st, P, pcp, bias, res, y, batch, h, w, Ho, Wo, \
+                       slope, post_op);                                                                      \
+    FVC_CHECK_LAUNCH();                                                                                      \
+    return 0;                                                                                                \
+  }
+  FVC_TG(3, 1, 0) FVC_TG(3, 2, 0) FVC_TG(3, 3, 0) FVC_TG(3, 4, 0)
+  FVC_TG(5, 1, 0) FVC_TG(5, 2, 0) FVC_TG(5, 3, 0) FVC_TG(5, 4, 0)
+  FVC_TG(3, 1, 1) FVC_TG(3, 2, 1) FVC_TG(3, 3, 1) FVC_TG(3, 4, 1)
+  FVC_TG(5, 1, 1) FVC_TG(5, 2, 1) FVC_TG(5, 3, 1) FVC_TG(5, 4, 1)
+#undef FVC_TG
+  return FVC_EINVAL;
 }
 
 int fvc_sub_f32(const float* a, const float* b, float* out, size_t n, fvc_stream_t s) {

@@ -6,6 +6,8 @@ kernels trust their arguments (an out-of-bounds launch can fault the whole GPU).
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import _lib, profiling
@@ -157,6 +159,24 @@ class PackedConv:
         else:
             cout, cin = w.shape[0], w.shape[1]
         precision = precision or conv_precision()
+        self.cin, self.cout, self.ksize, self.stride, self.transposed = cin, cout, ksize, stride, transposed
+        # cout <= 4 with a wide input (mvDecoder deconv8, 128->2 3x3): N padded to a 32-wide MFMA
+        # tile wastes 16x, so the layer runs as a 1x1 x3 GEMM to N' = k*k*cout tap partials per
+        # input pixel + fvc_tap_gather_nhwc (0.66 -> 0.47 ms at 1080p). For 64 input channels
+        # (Warp_net conv6, resDecoder deconv4) the direct x3 kernel is faster (0.31 vs 0.43 ms,
+        # 0.24 vs 0.35 ms), so they stay direct. FVC_TAPSUM=0 / 2 disables / forces the tap path
+        # for every eligible layer.
+        self.tap = None
+        tapsum = os.environ.get("FVC_TAPSUM", "1")
+        if (precision == "x3" and cout <= 4 and ksize in (3, 5) and stride == (2 if transposed else 1)
+                and cp4(cin) % 8 == 0 and tapsum != "0" and (tapsum == "2" or (cin >= 128 and not transposed))):
+            nt = ksize * ksize
+            wt = w.permute(2, 3, 1, 0) if transposed else w.permute(2, 3, 0, 1)  # [ky][kx][co][ci]
+            self.tap = PackedConv(wt.reshape(nt * cout, cin, 1, 1).contiguous(), torch.zeros(nt * cout), 1, 1,
+                                  False, device, precision="x3")
+            self.x3 = self.tap.x3
+            self.bias = bias.detach().to(device, torch.float32).contiguous()
+            return
         self.x3 = precision == "x3" and bool(lib.fvc_conv_x3_supported(cin, cout, ksize, stride, int(transposed)))
         if self.x3:
             nbytes = lib.fvc_conv_x3_wpack_bytes(cin, cout, ksize, stride, int(transposed))
@@ -174,7 +194,6 @@ class PackedConv:
                       int(transposed))
         self.wpack = packed.to(device)
         self.bias = bias.detach().to(device, torch.float32).contiguous()
-        self.cin, self.cout, self.ksize, self.stride, self.transposed = cin, cout, ksize, stride, transposed
 
     def out_hw(self, h, w):
         if self.transposed:
@@ -193,6 +212,11 @@ class PackedConv:
         _chk(res, oshape, name="res")
         y = out if out is not None else torch.empty(oshape, dtype=torch.float32, device=x.device)
         _chk(y, oshape, name="y")
+        if self.tap is not None:
+            P = self.tap(x, in_op=in_op)  # timed (if a KernelTimer is active) as an x3 launch
+            _lib.call("fvc_tap_gather_nhwc", P.data_ptr(), P.shape[-1], self.bias.data_ptr(), _ptr(res), y.data_ptr(),
+                      B, H, W, self.cout, self.ksize, self.stride, int(self.transposed), act, post, stream_handle())
+            return y
         timer = profiling.active()
         if timer is not None:
             ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

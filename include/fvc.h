@@ -120,6 +120,17 @@ int fvc_mc_assemble(const float* ref, const float* mv, float* warpframe, float* 
 /* out = a - b elementwise over n floats */
 int fvc_sub_f32(const float* a, const float* b, float* out, size_t n, fvc_stream_t stream);
 
+/* cout <= 4 conv (stride 1) / transposed conv (stride 2) as a tap-partial GEMM: P [batch,h,w,pcp]
+ * holds, per input pixel, sum_ci x * w for every tap t = ky*ksize+kx and output channel co at
+ * channel t*cout+co (a 1x1 fvc_conv2d_nhwc_x3 with cout' = ksize^2 * cout); this sums the taps
+ * reaching each output pixel, adds bias, applies act / res / post_op, writes y [.., 4] (pad = 0).
+ * Replaces the same nn.Conv2d / nn.ConvTranspose2d forwards as fvc_conv2d_nhwc_* for the 2- and
+ * 3-channel output layers (DVC/subnet/endecoder.py:279,295 Warp_net.conv6; synthesis_mv.py:43
+ * deconv8; synthesis.py:26,57 deconv4). */
+int fvc_tap_gather_nhwc(const float* P, int pcp, const float* bias, const float* res, float* y, int batch,
+                        int h, int w, int cout, int ksize, int stride, int transposed, int act, int post_op,
+                        fvc_stream_t stream);
+
 /* ------------------------------------------------------------------ GDN (GDN.py:63-93)
  * beta/gamma are the effective (bounded, reparametrised) parameters: gamma[i*c + j] */
 int fvc_gdn_nhwc(const float* x, float* y, const float* beta, const float* gamma, int batch,

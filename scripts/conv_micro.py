@@ -28,6 +28,10 @@ CASES = {
     "c3_64_3_full": (64, 3, 3, 1, False, 1088, 1920),
     "d5_64_3_half": (64, 3, 5, 2, True, 1088, 1920),
     "c7_16_2_full": (16, 2, 7, 1, False, 1088, 1920),
+    # tap-partial GEMMs of the cout <= 4 layers (kernels.PackedConv tap path)
+    "c1_128_18_full": (128, 18, 1, 1, False, 1088, 1920),
+    "c1_64_27_full": (64, 27, 1, 1, False, 1088, 1920),
+    "c1_64_75_half": (64, 75, 1, 1, False, 544, 960),
     # Warp_net ResBlock second conv: relu on the input, residual add in the epilogue
     "c3_64_full_res": (64, 64, 3, 1, False, 1088, 1920, "res"),
     "c3_64_half_res": (64, 64, 3, 1, False, 544, 960, "res"),

@@ -119,6 +119,31 @@ def test_conv_x3_weight_paths_identical(dev, case, monkeypatch):
     assert torch.equal(outs[0], outs[1])
 
 
+@pytest.mark.parametrize("case", [CONV_CASES[i] for i in (9, 12, 19)],
+                         ids=lambda c: f"ci{c[0]}co{c[1]}k{c[2]}s{c[3]}{'T' if c[4] else ''}")
+def test_conv_tap_partial_path(dev, case, monkeypatch):
+    """cout <= 4 layers as a 1x1 x3 GEMM to k*k*cout tap partials + fvc_tap_gather_nhwc (forced
+    for every eligible geometry with FVC_TAPSUM=2) against the fp32 torch conv."""
+    monkeypatch.setenv("FVC_TAPSUM", "2")
+    cin, cout, k, s, tr, H, W, in_op, act, post, with_res = case
+    g = torch.Generator().manual_seed(cin + 31 * cout)
+    x = torch.randn(2, cin, H, W, generator=g) * 2.0
+    w = torch.randn((cin, cout, k, k) if tr else (cout, cin, k, k), generator=g) * (1.0 / (cin * k * k) ** 0.5)
+    b = torch.randn(cout, generator=g) * 0.1
+    xin = _in_op(x, in_op)
+    ref = F.conv_transpose2d(xin, w, b, s, k // 2, s - 1) if tr else F.conv2d(xin, w, b, s, k // 2)
+    res = torch.randn(ref.shape, generator=g) if with_res else None
+    if res is not None:
+        ref = ref + res
+    pc = K.PackedConv(w, b, k, s, tr, dev, precision="x3")
+    assert pc.tap is not None
+    y = pc(to_nhwc(x).to(dev), in_op=in_op, act=act, post=post, res=None if res is None else to_nhwc(res).to(dev))
+    torch.cuda.synchronize()
+    yc = y.cpu()
+    close(from_nhwc(yc, cout), ref, 2e-5)
+    assert float(yc[..., cout:].abs().max()) == 0.0
+
+
 def test_conv_x3_overflow_flag(dev):
     """|activation| >= 65000 cannot be split into fp16 halves: the x3 kernel must flag it."""
     w = torch.randn(64, 64, 3, 3) * 0.05
