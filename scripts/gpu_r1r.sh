@@ -2,7 +2,7 @@
 # Round-1 evidence pass: GPU parity suite, default bench (with CPU baseline), rocprofv3 kernel
 # trace/stats of the serial bench, FETCH_SIZE and WRITE_SIZE passes (separate runs).
 export TMPDIR=/tmp
-O=gpurun_out/r1r
+O=gpurun_out/${1:-r1r}
 mkdir -p $O
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { tail -40 $O/pytest_gpu.log; exit 1; }
 tail -2 $O/pytest_gpu.log
