@@ -34,9 +34,36 @@ def _side_streams(device):
     return _STREAMS[key]
 
 
-def encode_decode_gop(model, frames: torch.Tensor, check=False, overlap=True):
+def _record(obj, stream, seen=None):
+    """record_stream every tensor reachable from obj (dicts, sequences, plain objects) on stream,
+    so the caching allocator does not hand its memory out again before that stream's use ends."""
+    seen = set() if seen is None else seen
+    if id(obj) in seen:
+        return
+    seen.add(id(obj))
+    if isinstance(obj, torch.Tensor):
+        if obj.is_cuda:
+            obj.record_stream(stream)
+    elif isinstance(obj, dict):
+        for v in obj.values():
+            _record(v, stream, seen)
+    elif isinstance(obj, (list, tuple)):
+        for v in obj:
+            _record(v, stream, seen)
+    elif hasattr(obj, "__dict__"):
+        for v in vars(obj).values():
+            _record(v, stream, seen)
+
+
+def encode_decode_gop(model, frames: torch.Tensor, check=False, overlap=True, join=True):
     """frames: [G, T, 3, H, W] device tensor. Returns (bitstreams, decoder recons, encoder sse
-    list, encoder recons); every returned tensor is ready on the caller's stream."""
+    list, encoder recons); with join=True every returned tensor is ready on the caller's stream.
+
+    join=False (streaming use, e.g. back-to-back GOPs in bench.py): the caller's stream does not
+    wait for this GOP's coder/decoder tail, so the next GOP's encoder starts while the last
+    frames are still being range-decoded and reconstructed; every tensor that crosses streams is
+    record_stream'ed, and the caller synchronises the device (or waits on the side streams via
+    join_side_streams) before reading the returned bitstreams / recons."""
     G, T = frames.shape[:2]
     main = torch.cuda.current_stream(frames.device)
     if overlap:
@@ -64,12 +91,25 @@ def encode_decode_gop(model, frames: torch.Tensor, check=False, overlap=True):
             s_rec.wait_stream(s_ed)
             with torch.cuda.stream(s_rec):
                 rec_dec = model.reconstruct(dlat, x_dec)
+            if overlap and not join:
+                if t == 1:
+                    _record(x_enc, s_rec)  # the I-frame: decoder reference of frame 1
+                _record(lat, s_code)
+                _record(bs, s_ed)
+                _record(dlat, s_rec)
             keep.append((lat, cur, dlat))  # cross-stream tensors stay alive until the pipeline drains
             bitstreams.append(bs)
             decoded.append(rec_dec)
             enc_recons.append(clipped)
             sses.append(sse)
             x_enc, x_dec = clipped, rec_dec
-    for st in {s_code, s_ed0, s_ed1, s_rec}:
-        main.wait_stream(st)
+    if join:
+        join_side_streams(frames.device)
     return bitstreams, decoded, sses, enc_recons
+
+
+def join_side_streams(device):
+    """Make the current stream wait for all pipeline side streams of device."""
+    main = torch.cuda.current_stream(device)
+    for st in _side_streams(device):
+        main.wait_stream(st)

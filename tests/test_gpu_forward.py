@@ -244,3 +244,23 @@ def test_forward_vs_oracle_1080p(model, dev):
         assert report[name] <= 1e-2, report
     assert report["dpsnr_db"] <= 1e-3, report
     assert report["bpp_rel"] <= 1e-3, report
+
+
+def test_gop_streaming_back_to_back(model, dev):
+    """join=False (bench.py's timed loop): three GOPs enqueued back to back, each next GOP's
+    encoder overlapping the previous GOP's coder/decoder tail. Every GOP must still decode to its
+    encoder's recon bit-for-bit and equal a joined run (no allocator reuse across streams)."""
+    from fastvideocodec_amd.gop import encode_decode_gop
+    from fastvideocodec_amd.synthetic import make_gop
+    gops = [torch.from_numpy(np.stack([make_gop(128, 192, 5, 40 + g)])).to(dev) for g in range(3)]
+    ref = [encode_decode_gop(model, f, overlap=True, join=True) for f in gops]
+    torch.cuda.synchronize()
+    ref = [([b.feature.to_bytes_list() for b in r[0]], [d.clone() for d in r[1]]) for r in ref]
+    outs = [encode_decode_gop(model, f, overlap=True, join=False) for f in gops]
+    torch.cuda.synchronize()
+    for (bss, dec, _, enc), (rb, rd) in zip(outs, ref):
+        for a, b in zip(dec, enc):
+            assert torch.equal(a, b)
+        for a, b in zip(dec, rd):
+            assert torch.equal(a, b)
+        assert [b.feature.to_bytes_list() for b in bss] == rb
