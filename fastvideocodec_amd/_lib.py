@@ -29,6 +29,7 @@ _SIGS = {
     "fvc_conv_x3_pack_weight": (c_int, [vp, vp, vp] + [c_int] * 5),
     "fvc_conv2d_nhwc_x3": (c_int, [vp, vp, c_float, vp, vp, vp] + [c_int] * 10 + [vp]),
     "fvc_deconv2d_nhwc_x3": (c_int, [vp, vp, c_float, vp, vp, vp] + [c_int] * 10 + [vp]),
+    "fvc_x3_set_cu_reserve": (c_int, [c_int]),
     "fvc_x3_overflow_flag": (c_int, [vp, c_int]),
     "fvc_nchw_to_nhwc": (c_int, [vp, vp, c_int, c_int, c_int, c_int, c_int, vp]),
     "fvc_nhwc_to_nchw": (c_int, [vp, vp, c_int, c_int, c_int, c_int, c_int, c_int, vp]),

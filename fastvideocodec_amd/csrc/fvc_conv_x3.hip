@@ -760,6 +760,8 @@ static bool x3_cfg(int cin, int cout, int ks, int stride, int transposed, X3Cfg&
   return true;
 }
 
+static int g_x3_reserve = 0;  // fvc_x3_set_cu_reserve
+
 static int x3_num_cus() {
   static int n = 0;
   if (!n) {
@@ -926,7 +928,11 @@ static int run_x3(const float* x, const void* wpack, float osc, const float* bia
     while (wn > 1 && base * (c.ntp / wn) < 2LL * x3_num_cus()) wn >>= 1;
   // persistent grid: ~one 8-wave block per CU (FVC_X3_BPC blocks per CU), each walking a
   // contiguous run of spatial tiles
-  const int ncu = x3_num_cus();
+  // FVC_X3_RESERVE CUs are left out of the persistent grid for kernels of other streams (the
+  // latency-bound rANS chains): a block that cannot find a free CU would start only when another
+  // block has finished its whole run, doubling the launch's time
+  const int reserve = env_int("FVC_X3_RESERVE", -1) >= 0 ? env_int("FVC_X3_RESERVE", 0) : g_x3_reserve;
+  const int ncu = x3_num_cus() - (reserve < x3_num_cus() / 2 ? reserve : x3_num_cus() / 2);
   const long long yz = (long long)(c.ntp / wn) * batch;
   const int bpc = env_int("FVC_X3_BPC", 1);
   long long gx = ((long long)ncu * bpc + yz - 1) / yz;  // blocks over all (tile, class) items
@@ -1022,6 +1028,12 @@ int fvc_deconv2d_nhwc_x3(const float* x, const void* wpack, float osc, const flo
                          fvc_stream_t stream) {
   return run_x3(x, wpack, osc, bias, res, y, batch, h, w, cin, cout, ksize, stride, 1, in_op, act,
                 post_op, (hipStream_t)stream);
+}
+
+int fvc_x3_set_cu_reserve(int ncu) {
+  if (ncu < 0) return FVC_EINVAL;
+  g_x3_reserve = ncu;
+  return 0;
 }
 
 int fvc_x3_overflow_flag(int* host_flag, int reset) {

@@ -20,9 +20,16 @@ G GOPs are batched along dim 0 (frame t of every GOP in one forward).
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
+from . import _lib
 from . import kernels as K
+
+# CUs the conv kernels' persistent grids leave free while the pipeline's side streams run
+# (measured on MI355X, bench.py: 0 -> 37.4, 32 -> 38.7, 48 -> 38.7, 96 -> 36.7 P-frames/s)
+PIPELINE_CU_RESERVE = int(os.environ.get("FVC_PIPELINE_CU_RESERVE", "40"))
 
 _STREAMS = {}
 
@@ -70,6 +77,7 @@ def encode_decode_gop(model, frames: torch.Tensor, check=False, overlap=True, jo
         s_code, s_ed0, s_ed1, s_rec = _side_streams(frames.device)
     else:
         s_code = s_ed0 = s_ed1 = s_rec = main
+    _lib.call("fvc_x3_set_cu_reserve", PIPELINE_CU_RESERVE if overlap else 0)
     x_enc = frames[:, 0].contiguous()
     x_dec = x_enc
     bitstreams, decoded, sses, enc_recons, keep = [], [], [], [], [x_enc]
@@ -103,6 +111,7 @@ def encode_decode_gop(model, frames: torch.Tensor, check=False, overlap=True, jo
             enc_recons.append(clipped)
             sses.append(sse)
             x_enc, x_dec = clipped, rec_dec
+    _lib.call("fvc_x3_set_cu_reserve", 0)  # launches outside the pipeline get the whole GPU
     if join:
         join_side_streams(frames.device)
     return bitstreams, decoded, sses, enc_recons

@@ -92,6 +92,12 @@ int fvc_deconv2d_nhwc_x3(const float* x, const void* wpack, float osc, const flo
                          int ksize, int stride, int in_op, int act, int post_op,
                          fvc_stream_t stream);
 int fvc_x3_overflow_flag(int* host_flag, int reset);
+/* CUs the split-precision conv's persistent grid leaves to kernels of other streams (default 0;
+ * capped at half the CUs). A pipelined caller (encoder + coder + decoder streams in flight, see
+ * fastvideocodec_amd/gop.py) sets it so that a conv block never waits for a CU held by a
+ * long-running rANS chain, which would double that launch's time. Host-side setting, applies to
+ * subsequent launches. */
+int fvc_x3_set_cu_reserve(int ncu);
 
 /* ------------------------------------------------------------------ layout / resampling */
 int fvc_nchw_to_nhwc(const float* src, float* dst, int batch, int c, int h, int w, int cp,
