@@ -2,14 +2,15 @@
 models.py:368-383): the I-frame passes through (BPG out of scope), every P-frame is encoded and
 then decoded from its bitstream.
 
-Four kinds of HIP streams form a pipeline:
+Four HIP streams form a pipeline (four, because the GPU exposes GPU_MAX_HW_QUEUES = 4 hardware
+queues per process: a fifth stream would share a queue and serialise behind another stream's
+work):
   * encoder stream (the caller's current stream): the encoder forward of frame t, using the
     encoder's own reconstruction of frame t-1 as reference (exactly what the reference loop
     does: x_prev = model(...)[0]);
-  * coder stream: symbols -> rANS encode of frame t (waits only on frame t's latents);
-  * entropy-decode streams (two, round-robin over frames): rANS decode of frame t's z ->
-    hyperprior -> feature, and mv (waits only on frame t's bitstream; no reference frame needed,
-    so consecutive frames decode concurrently);
+  * two coder streams, round-robin over frames: symbols -> rANS encode of frame t (waits only on
+    frame t's latents), then rANS decode of its z -> hyperprior -> feature, and mv (no reference
+    frame needed, so consecutive frames code and decode concurrently);
   * reconstruction stream: mvDecoder + motion compensation + resDecoder of frame t against the
     decoder's own previous reconstruction (waits on frame t's latents).
 Encoder and decoder reconstructions are bit-identical (same kernels, same operand order;
@@ -37,7 +38,7 @@ _STREAMS = {}
 def _side_streams(device):
     key = str(device)
     if key not in _STREAMS:
-        _STREAMS[key] = tuple(torch.cuda.Stream(device=device) for _ in range(4))
+        _STREAMS[key] = tuple(torch.cuda.Stream(device=device) for _ in range(3))
     return _STREAMS[key]
 
 
@@ -74,9 +75,9 @@ def encode_decode_gop(model, frames: torch.Tensor, check=False, overlap=True, jo
     G, T = frames.shape[:2]
     main = torch.cuda.current_stream(frames.device)
     if overlap:
-        s_code, s_ed0, s_ed1, s_rec = _side_streams(frames.device)
+        s_cd0, s_cd1, s_rec = _side_streams(frames.device)
     else:
-        s_code = s_ed0 = s_ed1 = s_rec = main
+        s_cd0 = s_cd1 = s_rec = main
     _lib.call("fvc_x3_set_cu_reserve", PIPELINE_CU_RESERVE if overlap else 0)
     x_enc = frames[:, 0].contiguous()
     x_dec = x_enc
@@ -89,21 +90,18 @@ def encode_decode_gop(model, frames: torch.Tensor, check=False, overlap=True, jo
             clipped, sse = K.recon_finalize(tens["recon"], tens["cur4"], tens["warpframe"], tens["prediction"])
             lat = {k: tens[k] for k in ("mvfeature", "z", "feature", "sigma")}
             del tens
-            s_code.wait_stream(main)
-            with torch.cuda.stream(s_code):
+            s_cd = s_cd0 if t % 2 else s_cd1
+            s_cd.wait_stream(main)
+            with torch.cuda.stream(s_cd):
                 bs = model.compress_tensors(lat)
-            s_ed = s_ed0 if t % 2 else s_ed1
-            s_ed.wait_stream(s_code)
-            with torch.cuda.stream(s_ed):
                 dlat = model.decode_latents(bs, check=check)
-            s_rec.wait_stream(s_ed)
+            s_rec.wait_stream(s_cd)
             with torch.cuda.stream(s_rec):
                 rec_dec = model.reconstruct(dlat, x_dec)
             if overlap and not join:
                 if t == 1:
                     _record(x_enc, s_rec)  # the I-frame: decoder reference of frame 1
-                _record(lat, s_code)
-                _record(bs, s_ed)
+                _record(lat, s_cd)
                 _record(dlat, s_rec)
             keep.append((lat, cur, dlat))  # cross-stream tensors stay alive until the pipeline drains
             bitstreams.append(bs)
