@@ -36,6 +36,7 @@ from fastvideocodec_amd.gop import encode_decode_gop  # noqa: E402
 from fastvideocodec_amd.models import get_codec_model  # noqa: E402
 from fastvideocodec_amd.synthetic import gop_seed, make_gop  # noqa: E402
 
+HBM_PEAK_BPS = 8.0e12           # MI355X_MICROARCH.md: HBM3E peak (spec; ~6.3 TB/s achievable)
 F16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16/F16 dense matrix peak (~2.5 PF)
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 matrix (v_mfma_f32_32x32x2_f32), dense
 ENC_TFLOP_PER_PFRAME = 2.931   # SURVEY.md §8(d) algorithmic, 1920x1088
@@ -66,7 +67,23 @@ def cpu_baseline(H, W, frames_np):
         nbytes += len(R.CRef.encode(feat[0, c].ravel(), idx[0, c].ravel(), lt.cdf, lt.cdf_length, lt.offset))
     dvc_ref.decode(sd, ref, inter["quant_mv"], inter["compressed_z"], inter["compressed_feature"])
     dt = time.perf_counter() - t0
+    # also one thread on config 1's 256x256 pair (oracle forward only)
+    from fastvideocodec_amd.synthetic import make_gop
+    small = make_gop(256, 256, 2, 20261015)
+    torch.set_num_threads(1)
+    c1, r1 = torch.from_numpy(small[1:2].copy()), torch.from_numpy(small[0:1].copy())
+    dvc_ref.forward(sd, c1, r1)  # warm
+    t1 = time.perf_counter()
+    dvc_ref.forward(sd, c1, r1)
+    dt1 = time.perf_counter() - t1
+    torch.set_num_threads(cores)
+    cpu_model = ""
+    try:
+        cpu_model = next(l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name"))
+    except (OSError, StopIteration):
+        pass
     return {"value": round(1.0 / dt, 4), "unit": "P-frames/s", "cores": cores, "kind": "port",
+            "cpu": cpu_model, "one_thread_256x256_forward_s": round(dt1, 3),
             "sample": f"1 P-frame {W}x{H}: oracle forward (encode+recon) + oracle decode + C rANS of the "
                       f"feature latent, torch CPU fp32, {dt:.1f} s",
             "seconds": round(dt, 2)}
@@ -147,6 +164,7 @@ def main():
     conv_ms, conv_flops, n_launch = timer.collect()
     x3_ms, x3_flops, x3_launch = timer.collect(x3=True)
     x3_bytes = timer.collect_bytes(x3=True)
+    hbm = timer.collect_hbm()
     if args.breakdown and rank == 0:
         agg = timer.breakdown()
         for k, (n, ms, fl) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
@@ -215,6 +233,11 @@ def main():
                                    "gflop_per_pframe": round(conv_flops / nfr / 1e9, 1),
                                    "tflops": round(conv_flops / (conv_ms * 1e-3) / 1e12, 2) if conv_ms else 0.0,
                                    "launches": n_launch}},
+        "hbm_kernels": {k: {"gb_per_s": round(b / (ms * 1e-3) / 1e9, 1) if ms else None,
+                            "frac_of_8tbps": round(b / (ms * 1e-3) / HBM_PEAK_BPS, 4) if ms else None,
+                            "ms_per_pframe": round(ms / nfr, 3), "gb_per_pframe": round(b / nfr / 1e9, 3),
+                            "launches": n}
+                        for k, (n, ms, b) in sorted(hbm.items(), key=lambda kv: -kv[1][1])},
         "quality": {"decoder_bitexact": bitexact_all, "bytes_per_pframe": round(bytes_all / (G * (args.gop - 1) * world), 1),
                     "bpp_actual": round(bytes_all * 8 / (G * (args.gop - 1) * world * Hp * Wp), 5),
                     "psnr_db_mean": round(psnr_all, 4),

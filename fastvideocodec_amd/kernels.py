@@ -68,7 +68,8 @@ def avgpool2(x: torch.Tensor) -> torch.Tensor:
     B, H, W, cp = x.shape
     _chk(x, name="x")
     y = torch.empty((B, H // 2, W // 2, cp), dtype=torch.float32, device=x.device)
-    _lib.call("fvc_avgpool2_nhwc", x.data_ptr(), y.data_ptr(), B, H, W, cp, stream_handle())
+    profiling.timed_hbm("avgpool2", 4 * (x.numel() + y.numel()), lambda: _lib.call(
+        "fvc_avgpool2_nhwc", x.data_ptr(), y.data_ptr(), B, H, W, cp, stream_handle()))
     return y
 
 
@@ -86,8 +87,10 @@ def upsample2x_add(src, skip=None, align_corners=True, scale=1.0):
     _chk(src, name="src")
     _chk(skip, (B, 2 * h, 2 * w, cp), name="skip")
     y = torch.empty((B, 2 * h, 2 * w, cp), dtype=torch.float32, device=src.device)
-    _lib.call("fvc_upsample2x_add_nhwc", src.data_ptr(), _ptr(skip), y.data_ptr(), B, h, w, cp,
-              int(align_corners), float(scale), stream_handle())
+    nb = 4 * (src.numel() + y.numel() + (skip.numel() if skip is not None else 0))
+    profiling.timed_hbm("upsample2x_add", nb, lambda: _lib.call(
+        "fvc_upsample2x_add_nhwc", src.data_ptr(), _ptr(skip), y.data_ptr(), B, h, w, cp, int(align_corners),
+        float(scale), stream_handle()))
     return y
 
 
@@ -98,8 +101,11 @@ def spynet_assemble(im1, im2, flow_prev):
     _chk(flow_prev, (B, H // 2, W // 2, 4), name="flow_prev")
     flow_up = torch.empty((B, H, W, 4), dtype=torch.float32, device=im1.device)
     x8 = torch.empty((B, H, W, 8), dtype=torch.float32, device=im1.device)
-    _lib.call("fvc_spynet_assemble", im1.data_ptr(), im2.data_ptr(), _ptr(flow_prev), flow_up.data_ptr(),
-              x8.data_ptr(), B, H, W, stream_handle())
+    nb = 4 * (im1.numel() + im2.numel() + (flow_prev.numel() if flow_prev is not None else 0) + flow_up.numel()
+              + x8.numel())
+    profiling.timed_hbm("spynet_assemble (warp)", nb, lambda: _lib.call(
+        "fvc_spynet_assemble", im1.data_ptr(), im2.data_ptr(), _ptr(flow_prev), flow_up.data_ptr(), x8.data_ptr(), B,
+        H, W, stream_handle()))
     return flow_up, x8
 
 
@@ -109,8 +115,10 @@ def mc_assemble(ref, mv):
     _chk(mv, (B, H, W, 4), name="mv")
     warpframe = torch.empty((B, H, W, 4), dtype=torch.float32, device=ref.device)
     x8 = torch.empty((B, H, W, 8), dtype=torch.float32, device=ref.device)
-    _lib.call("fvc_mc_assemble", ref.data_ptr(), mv.data_ptr(), warpframe.data_ptr(), x8.data_ptr(), B, H, W,
-              stream_handle())
+    nb = 4 * (ref.numel() + mv.numel() + warpframe.numel() + x8.numel())
+    profiling.timed_hbm("mc_assemble (warp)", nb, lambda: _lib.call(
+        "fvc_mc_assemble", ref.data_ptr(), mv.data_ptr(), warpframe.data_ptr(), x8.data_ptr(), B, H, W,
+        stream_handle()))
     return warpframe, x8
 
 
@@ -128,8 +136,9 @@ def gdn(x, beta, gamma, inverse):
     _chk(beta, (C,), name="beta")
     _chk(gamma, (C, C), name="gamma")
     y = torch.empty_like(x)
-    _lib.call("fvc_gdn_nhwc", x.data_ptr(), y.data_ptr(), beta.data_ptr(), gamma.data_ptr(), B, H, W, C,
-              int(inverse), stream_handle())
+    profiling.timed_hbm("gdn", 4 * (x.numel() + y.numel()), lambda: _lib.call(
+        "fvc_gdn_nhwc", x.data_ptr(), y.data_ptr(), beta.data_ptr(), gamma.data_ptr(), B, H, W, C, int(inverse),
+        stream_handle()))
     return y
 
 
@@ -214,8 +223,10 @@ class PackedConv:
         _chk(y, oshape, name="y")
         if self.tap is not None:
             P = self.tap(x, in_op=in_op)  # timed (if a KernelTimer is active) as an x3 launch
-            _lib.call("fvc_tap_gather_nhwc", P.data_ptr(), P.shape[-1], self.bias.data_ptr(), _ptr(res), y.data_ptr(),
-                      B, H, W, self.cout, self.ksize, self.stride, int(self.transposed), act, post, stream_handle())
+            nb = 4 * (P.numel() + y.numel() * (2 if res is not None else 1))
+            profiling.timed_hbm("tap_gather", nb, lambda: _lib.call(
+                "fvc_tap_gather_nhwc", P.data_ptr(), P.shape[-1], self.bias.data_ptr(), _ptr(res), y.data_ptr(), B, H, W,
+                self.cout, self.ksize, self.stride, int(self.transposed), act, post, stream_handle()))
             return y
         timer = profiling.active()
         if timer is not None:
@@ -270,8 +281,11 @@ def recon_finalize(recon, inp, warpframe, prediction):
         _chk(t, (B, H, W, 4), name=n)
     clipped = torch.empty((B, 3, H, W), dtype=torch.float32, device=recon.device)
     out3 = torch.empty(3, dtype=torch.float64, device=recon.device)
-    _lib.call("fvc_recon_finalize", recon.data_ptr(), inp.data_ptr(), warpframe.data_ptr(), prediction.data_ptr(),
-              clipped.data_ptr(), out3.data_ptr(), _ws(recon.device).data_ptr(), B, H, W, stream_handle())
+    nb = 4 * (recon.numel() + inp.numel() + warpframe.numel() + prediction.numel() + clipped.numel())
+    ws = _ws(recon.device)
+    profiling.timed_hbm("recon_finalize", nb, lambda: _lib.call(
+        "fvc_recon_finalize", recon.data_ptr(), inp.data_ptr(), warpframe.data_ptr(), prediction.data_ptr(),
+        clipped.data_ptr(), out3.data_ptr(), ws.data_ptr(), B, H, W, stream_handle()))
     return clipped, out3
 
 

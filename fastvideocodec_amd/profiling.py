@@ -23,6 +23,7 @@ def conv_flops(cin, cout, k, stride, transposed, batch, h, w):
 class KernelTimer:
     def __init__(self):
         self.records = []
+        self.hbm_records = []  # (ev0, ev1, name, algorithmic bytes) of the HBM-bound kernels
 
     def __enter__(self):
         global _ACTIVE
@@ -47,6 +48,17 @@ class KernelTimer:
         ``collect(x3)`` counts."""
         return sum(r[5] for r in self.records if len(r) > 5 and (x3 is None or r[4] == x3))
 
+    def collect_hbm(self):
+        """{name: [launches, ms, algorithmic bytes]} of the HBM-bound (non-conv) kernels."""
+        torch.cuda.synchronize()
+        agg = {}
+        for ev0, ev1, name, nbytes in self.hbm_records:
+            a = agg.setdefault(name, [0, 0.0, 0.0])
+            a[0] += 1
+            a[1] += ev0.elapsed_time(ev1)
+            a[2] += nbytes
+        return agg
+
     def breakdown(self):
         """Per-geometry aggregate: {key: [launches, ms, flops]} (keys recorded by the caller)."""
         torch.cuda.synchronize()
@@ -62,3 +74,18 @@ class KernelTimer:
 
 def active():
     return _ACTIVE
+
+
+def timed_hbm(name, nbytes, fn):
+    """Run fn (one HBM-bound kernel launch); with a KernelTimer active, bracket it with HIP events
+    on the current stream and record its algorithmic bytes (each input read once, each output
+    written once, padded channels included: they are moved)."""
+    t = _ACTIVE
+    if t is None:
+        return fn()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record()
+    r = fn()
+    ev1.record()
+    t.hbm_records.append((ev0, ev1, name, float(nbytes)))
+    return r
