@@ -264,3 +264,23 @@ def test_gop_streaming_back_to_back(model, dev):
         for a, b in zip(dec, rd):
             assert torch.equal(a, b)
         assert [b.feature.to_bytes_list() for b in bss] == rb
+
+
+def test_4k_pframe_compress_decompress(model, dev):
+    """BASELINE configs[3] frame size (3840x2160, replicate-padded to 3840x2176): one P-frame
+    encodes, decodes bit-exactly to the encoder's recon, stays inside the split-precision range,
+    and its bits-estimate bpp is close to the real bitstream's."""
+    from fastvideocodec_amd import kernels as K
+    from fastvideocodec_amd.synthetic import make_gop, gop_seed
+    frames = torch.from_numpy(make_gop(2160, 3840, 2, gop_seed(3))).to(dev)
+    assert frames.shape[-2:] == (2176, 3840)
+    K.x3_overflow(reset=True)
+    bs, rec_enc = model.compress(frames[1:2], frames[0:1])
+    rec_dec = model.decompress(bs, frames[0:1])
+    out = model(frames[1:2], frames[0:1])
+    torch.cuda.synchronize()
+    assert not K.x3_overflow(reset=True)
+    assert torch.equal(rec_enc, rec_dec)
+    assert torch.equal(out[0], rec_enc)
+    real_bpp = bs.nbytes() * 8 / (2176 * 3840)
+    assert abs(real_bpp - float(out[7])) <= 0.02 * float(out[7]) + 1e-3, (real_bpp, float(out[7]))
