@@ -126,7 +126,8 @@ __device__ __forceinline__ void split8(const float (&v)[8], h8& hi, h8& lo, floa
 }
 
 // DBG (ablation builds only, scripts/gpu_x3_ablate.sh; 0 in the product): bit 0 no staging of
-// later chunks, bit 1 no weight loads in the k-loop, bit 2 no output stores, bit 3 no A LDS reads
+// later chunks, bit 1 no weight loads in the k-loop, bit 2 no output stores, bit 3 no A LDS reads,
+// bit 4 output stores issued with an out-of-range offset (dropped by the buffer range check)
 template <int CC, int WM, int WN, int NW, int IOP, int BL, int DBG = 0>
 __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(const X3Args a) {
   constexpr int C8 = CC / 8;
@@ -628,7 +629,7 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(const X3Args a) {
         }
 #pragma unroll
         for (int i = 0; i < 4; ++i) v[i] = j0 + i < a.cout ? v[i] : 0.f;  // pad channels = 0
-        const unsigned so = (row_ok && j0 < a.coutp) ? vo + 32u * g : kOob;
+        const unsigned so = ((DBG & 16) == 0 && row_ok && j0 < a.coutp) ? vo + 32u * g : kOob;
         if constexpr (DBG & 4) {
           asm volatile("" ::"v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]), "v"(so));
         } else {
@@ -813,6 +814,7 @@ static int x3_launch_t(const X3Args& a, dim3 grid, size_t lds, hipStream_t s) {
       case 3: return x3_launch_d<CC, WM, WN, IOP, BL, 3>(a, grid, lds, s);
       case 15: return x3_launch_d<CC, WM, WN, IOP, BL, 15>(a, grid, lds, s);
       case 11: return x3_launch_d<CC, WM, WN, IOP, BL, 11>(a, grid, lds, s);
+      case 16: return x3_launch_d<CC, WM, WN, IOP, BL, 16>(a, grid, lds, s);
       default: break;
     }
   }
