@@ -138,10 +138,13 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(const X3Args a) {
 
   extern __shared__ __attribute__((aligned(16))) _Float16 smh[];
   const int tile_h = 2 * C8 * a.ps;  // halves per A buffer: 2*C8 planes (hi octets, lo octets)
-  _Float16* const tile0 = smh + 256;  // two buffers at tile0 and tile0 + tile_h (LDS pointers;
+  _Float16* const tile0 = smh + 512;  // two buffers at tile0 and tile0 + tile_h (LDS pointers;
                                       // no pointer array, which would degrade them to flat)
-  float* const sbias = reinterpret_cast<float*>(smh);  // [WN * 32] bias of this block's N-tiles
-  _Float16* const sdump = smh + 128;  // 32 B sink for staging writes of items past the tile
+  // LDS header (1 KB): bias of this block's N-tiles [WN * 32] floats at bytes 0..511, the staging
+  // sink at 512..543
+  float* const sbias = reinterpret_cast<float*>(smh);
+  static_assert(WN * 32 * 4 <= 512, "bias area");
+  _Float16* const sdump = smh + 256;  // 32 B sink for staging writes of items past the tile
   // BL: two weight buffers after the A buffers, each [k-step][N-tile][hi|lo][lane] uint4
   _Float16* const wlds0 = tile0 + 2 * tile_h;
 
@@ -743,7 +746,7 @@ static bool x3_cfg(int cin, int cout, int ks, int stride, int transposed, X3Cfg&
     c.th = c.nw * c.wm;
     const int ir = (c.th - 1) * c.sin + 1 + (c.dymax - c.dymin);
     const int ic = 31 * c.sin + 1 + (c.dxmax - c.dxmin);
-    const size_t lds = 512 + 2 * x3_tile_bytes(ir, ic, c.cc);
+    const size_t lds = 1024 + 2 * x3_tile_bytes(ir, ic, c.cc);
     if (lds <= 160 * 1024) break;
     if (c.cc > 8 && c.cinp % (c.cc / 2) == 0) c.cc /= 2;
     else if (c.wm > 1) c.wm /= 2;
@@ -850,6 +853,7 @@ static int x3_launch_cc(int wm, int wn, int bl, int iop, const X3Args& a, dim3 g
   if (wm == 2 && wn == 1) return x3_launch_bl<CC, 2, 1>(bl, iop, a, grid, lds, s);
   if (wm == 1 && wn == 2) return x3_launch_bl<CC, 1, 2>(bl, iop, a, grid, lds, s);
   if (wm == 1 && wn == 1) return x3_launch_bl<CC, 1, 1>(bl, iop, a, grid, lds, s);
+  if (wm == 1 && wn == 4) return x3_launch_bl<CC, 1, 4>(bl, iop, a, grid, lds, s);
   return FVC_EINVAL;
 }
 
@@ -915,15 +919,17 @@ static int run_x3(const float* x, const void* wpack, float osc, const float* bia
       }
       a.toff[cl][t] = off;
     }
-  size_t lds = 512 + 2 * x3_tile_bytes(a.ir, a.ic, c.cc);
+  size_t lds = 1024 + 2 * x3_tile_bytes(a.ir, a.ic, c.cc);
   if (lds > 160 * 1024) return FVC_EINVAL;
   const int tiles_x = fvc_cdiv(a.Wq, 32);
   const int tiles_y = fvc_cdiv(a.Hq, c.th);
   // N-tiles per block: 2 (each staged input element feeds 64 output channels) unless the layer
   // has too few spatial tiles x N-groups to give every CU of the persistent grid some work
-  int wn = c.ntp >= 2 ? 2 : 1;
+  // stride-2 convs (one strip per wave) with 4 N-tiles take all 128 channels per block: the
+  // input tile is staged once instead of twice (3x3 s2 128->128 at 544x960: 0.214 -> 0.191 ms)
+  int wn = (c.wm == 1 && !transposed && stride == 2 && c.ntp % 4 == 0) ? 4 : (c.ntp >= 2 ? 2 : 1);
   const int want_wn = env_int("FVC_X3_WN", 0);
-  if (want_wn == 1 || want_wn == 2) wn = want_wn;
+  if (want_wn == 1 || want_wn == 2 || (want_wn == 4 && c.wm == 1)) wn = want_wn;
   while (wn > 1 && c.ntp % wn) wn >>= 1;
   const long long base = (long long)tiles_x * tiles_y * batch * c.nclass;
   if (!want_wn)

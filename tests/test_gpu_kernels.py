@@ -144,6 +144,26 @@ def test_conv_tap_partial_path(dev, case, monkeypatch):
     assert float(yc[..., cout:].abs().max()) == 0.0
 
 
+@pytest.mark.parametrize("wn", ["1", "2", "4"])
+def test_conv_x3_ntile_groupings(dev, wn, monkeypatch):
+    """The stride-2 128->128 conv with 1, 2 or all 4 N-tiles per block (FVC_X3_WN; 4 is the
+    default at full size) against the fp32 torch conv; all three must give identical bits."""
+    monkeypatch.setenv("FVC_X3_WN", wn)
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(2, 128, 48, 96, generator=g)
+    w = torch.randn(128, 128, 3, 3, generator=g) * (1.0 / (128 * 9) ** 0.5)
+    b = torch.randn(128, generator=g) * 0.1
+    ref = F.leaky_relu(F.conv2d(x, w, b, 2, 1), 0.1)
+    pc = K.PackedConv(w, b, 3, 2, False, dev, precision="x3")
+    y = pc(to_nhwc(x).to(dev), act=K.ACT_LRELU)
+    torch.cuda.synchronize()
+    close(from_nhwc(y.cpu(), 128), ref, 2e-5)
+    monkeypatch.setenv("FVC_X3_WN", "1")
+    y1 = pc(to_nhwc(x).to(dev), act=K.ACT_LRELU)
+    torch.cuda.synchronize()
+    assert torch.equal(y, y1)
+
+
 def test_conv_x3_overflow_flag(dev):
     """|activation| >= 65000 cannot be split into fp16 halves: the x3 kernel must flag it."""
     w = torch.randn(64, 64, 3, 3) * 0.05
