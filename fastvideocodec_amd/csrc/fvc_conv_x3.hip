@@ -878,14 +878,16 @@ static int run_x3(const float* x, const void* wpack, float osc, const float* bia
   // y and res are addressed through buffer descriptors with 32-bit offsets: split batches whose
   // output tensor reaches 4 GB into launches over sub-batches
   const unsigned long long ybytes = (unsigned long long)batch * a.Ho * a.Wo * a.coutp * 4ull;
-  if (ybytes >= (1ull << 32) - 4096) {
+  const long long split_env = env_int("FVC_X3_SPLIT_BYTES", 0);  // tests: force the split path
+  const unsigned long long split_at = split_env > 0 ? (unsigned long long)split_env : (1ull << 32) - 4096;
+  if (ybytes >= split_at) {
     if (batch == 1) return FVC_EINVAL;
     const int b1 = batch / 2;
     const size_t xs = (size_t)h * w * c.cinp, ys = (size_t)a.Ho * a.Wo * a.coutp;
     int rc = run_x3(x, wpack, osc, bias, res, y, b1, h, w, cin, cout, ks, stride, transposed, in_op, act,
                     post_op, s);
     if (rc) return rc;
-    return run_x3(x + b1 * xs, wpack, osc, bias, res + b1 * ys, y + b1 * ys, batch - b1, h, w, cin, cout, ks,
+    return run_x3(x + b1 * xs, wpack, osc, bias, res ? res + b1 * ys : nullptr, y + b1 * ys, batch - b1, h, w, cin, cout, ks,
                   stride, transposed, in_op, act, post_op, s);
   }
   a.y_bytes = (unsigned)ybytes;

@@ -164,6 +164,24 @@ def test_conv_x3_ntile_groupings(dev, wn, monkeypatch):
     assert torch.equal(y, y1)
 
 
+@pytest.mark.parametrize("with_res", [False, True])
+def test_conv_x3_batch_split(dev, with_res, monkeypatch):
+    """Outputs >= 4 GB are computed as launches over sub-batches (32-bit buffer offsets); the
+    split (forced here at a small size with FVC_X3_SPLIT_BYTES) must give the same bits as one
+    launch, with and without a residual (a missing residual must stay missing in every part)."""
+    g = torch.Generator().manual_seed(9)
+    x = to_nhwc(torch.randn(5, 64, 20, 40, generator=g)).to(dev)
+    w = torch.randn(64, 64, 3, 3, generator=g) * 0.04
+    b = torch.randn(64, generator=g) * 0.1
+    res = to_nhwc(torch.randn(5, 64, 20, 40, generator=g)).to(dev) if with_res else None
+    pc = K.PackedConv(w, b, 3, 1, False, dev, precision="x3")
+    y1 = pc(x, in_op=K.IN_RELU, res=res)
+    monkeypatch.setenv("FVC_X3_SPLIT_BYTES", str(2 * 20 * 40 * 64 * 4))  # parts of <= 1 image
+    y2 = pc(x, in_op=K.IN_RELU, res=res)
+    torch.cuda.synchronize()
+    assert torch.equal(y1, y2)
+
+
 def test_conv_x3_overflow_flag(dev):
     """|activation| >= 65000 cannot be split into fp16 halves: the x3 kernel must flag it."""
     w = torch.randn(64, 64, 3, 3) * 0.05
