@@ -300,43 +300,6 @@ __global__ void k_sub(const float* __restrict__ a, const float* __restrict__ b, 
 
 // ------------------------------------------------------------------ GDN / IGDN (C = 64)
 // norm_i = beta_i + sum_j gamma[i][j] x_j^2 ; y = x / sqrt(norm) (or x * sqrt(norm))
-template <int C>
-__global__ __launch_bounds__(kBlk) void k_gdn(const float* __restrict__ x, float* __restrict__ y,
-                                              const float* __restrict__ beta, const float* __restrict__ gamma,
-                                              size_t npix, int inverse) {
-  __shared__ float sg[C * C];
-  __shared__ float sb[C];
-  for (int i = threadIdx.x; i < C * C; i += blockDim.x) sg[i] = gamma[i];
-  for (int i = threadIdx.x; i < C; i += blockDim.x) sb[i] = beta[i];
-  __syncthreads();
-  for (size_t p = grid_stride_start(); p < npix; p += (size_t)gridDim.x * blockDim.x) {
-    float xv[C], x2[C];
-    const float4* xs = reinterpret_cast<const float4*>(x + p * C);
-#pragma unroll
-    for (int k = 0; k < C / 4; ++k) {
-      const float4 v = xs[k];
-      xv[4 * k] = v.x; xv[4 * k + 1] = v.y; xv[4 * k + 2] = v.z; xv[4 * k + 3] = v.w;
-    }
-#pragma unroll
-    for (int j = 0; j < C; ++j) x2[j] = xv[j] * xv[j];
-    float4* ys = reinterpret_cast<float4*>(y + p * C);
-#pragma unroll
-    for (int k = 0; k < C / 4; ++k) {
-      float o[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int i = 4 * k + u;
-        float acc = sb[i];
-#pragma unroll
-        for (int j = 0; j < C; ++j) acc = __builtin_fmaf(sg[i * C + j], x2[j], acc);
-        const float nrm = sqrtf(acc);
-        o[u] = inverse ? xv[i] * nrm : xv[i] / nrm;
-      }
-      ys[k] = make_float4(o[0], o[1], o[2], o[3]);
-    }
-  }
-}
-
 // GDN / IGDN on the fp32 matrix cores. norm = conv1x1(x^2, gamma) + beta is a [32 px x 64] x
 // [64 x 64] product per 32-pixel group: 2 N-tiles x 32 v_mfma_f32_32x32x2_f32 (an exact fp32 FMA
 // chain per output). gamma^T fragments stay in 64 VGPRs for the whole kernel. Lane (p, h) loads
