@@ -538,8 +538,19 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(const X3Args a) {
           store(nxt, sp);
         } else {
           for (; staged < nst; ++staged) {
-            half_stage(tid + staged * NT, q, S0, S1);
-            half_plain(q + 1, S1, S0);
+            // the staged item's split + LDS write come after the pair's second half-step, so
+            // its HBM loads have two half-steps of MFMAs (both waves of the SIMD) to land behind
+            load(q + 1 < nq ? q + 1 : nq - 1, S1);
+            Stage st;
+            fetch(tid + staged * NT, s_tile, s_ch, st);
+            __builtin_amdgcn_sched_barrier(0);
+            mfmas(S0);
+            __builtin_amdgcn_sched_barrier(0);
+            load(q + 2 < nq ? q + 2 : nq - 1, S0);
+            __builtin_amdgcn_sched_barrier(0);
+            mfmas(S1);
+            __builtin_amdgcn_sched_barrier(0);
+            store(nxt, st);
             q += 2;
             for (int r = 1; r < spread; ++r, q += 2) {
               half_plain(q, S0, S1);
