@@ -29,8 +29,9 @@ from . import _lib
 from . import kernels as K
 
 # CUs the conv kernels' persistent grids leave free while the pipeline's side streams run
-# (measured on MI355X, bench.py: 0 -> 37.4, 32 -> 38.7, 48 -> 38.7, 96 -> 36.7 P-frames/s)
-PIPELINE_CU_RESERVE = int(os.environ.get("FVC_PIPELINE_CU_RESERVE", "40"))
+# (measured on MI355X, bench.py at 4 GOPs per step, scripts/gpu_reserve_sweep.sh: 16 -> 49.2,
+# 24 -> 50.3, 32 -> 51.1, 40 -> 50.4, 48 -> 49.4, 64 -> 48.7 P-frames/s)
+PIPELINE_CU_RESERVE = int(os.environ.get("FVC_PIPELINE_CU_RESERVE", "32"))
 
 _STREAMS = {}
 
