@@ -250,6 +250,17 @@ def test_avgpool(dev):
     close(from_nhwc(y.cpu(), 64), F.avg_pool2d(x, 2, 2), 1e-6)
 
 
+def test_upsample_avgpool_tall(dev):
+    # more output rows than one grid dimension holds (65535): the row loop strides past it
+    g = torch.Generator().manual_seed(4)
+    src = torch.randn(1, 3, 33000, 3, generator=g)
+    skip = torch.randn(1, 3, 66000, 6, generator=g)
+    y = K.upsample2x_add(to_nhwc(src).to(dev), to_nhwc(skip).to(dev), align_corners=False, scale=2.0)
+    close(from_nhwc(y.cpu(), 3), skip + dvc_ref.up2(src, False) * 2.0, 1e-6)
+    p = K.avgpool2(to_nhwc(skip).to(dev))
+    close(from_nhwc(p.cpu(), 3), F.avg_pool2d(skip, 2, 2), 1e-6)
+
+
 def test_spynet_assemble(dev):
     g = torch.Generator().manual_seed(3)
     im1, im2 = torch.rand(1, 3, 32, 48, generator=g), torch.rand(1, 3, 32, 48, generator=g)
