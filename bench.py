@@ -119,6 +119,9 @@ def main():
     ap.add_argument("--gops-per-gpu", type=int, default=4,
                     help="GOPs batched per rank per step (SURVEY §8(e)); default 4 x 2 steps = 8 GOPs per run "
                          "(§8(d)). Measured on MI355X: 1 -> 44.5, 2 -> 47.6, 4 -> 49.1 P-frames/s")
+    ap.add_argument("--views", type=int, default=0,
+                    help="BASELINE configs[4]: V camera views, one GOP stream each, view v -> rank v %% world "
+                         "(replaces --gops-per-gpu; the reference's MCVC couples views, DVC views are independent)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--breakdown", action="store_true", help="print per-conv-geometry timing to stderr")
@@ -136,9 +139,18 @@ def main():
 
     model = get_codec_model("DVC-pretrained", compression_level=2, device=dev)
     model.update()
-    G = args.gops_per_gpu
-    my_gops = fdist.shard_gops(world * G, rank, world)  # GOP g -> rank g % world
-    gops = [make_gop(args.height, args.width, args.gop, gop_seed(g)) for g in my_gops]
+    if args.views > 0:
+        # configs[4]: one GOP stream per camera view, view v -> rank v % world
+        if args.views < world:
+            raise SystemExit(f"--views {args.views} < world size {world}: a rank would have no view")
+        my_views = fdist.shard_views(args.views, rank, world)
+        gops = [make_gop(args.height, args.width, args.gop, gop_seed(0, v)) for v in my_views]
+        n_units = args.views
+    else:
+        my_gops = fdist.shard_gops(world * args.gops_per_gpu, rank, world)  # GOP g -> rank g % world
+        gops = [make_gop(args.height, args.width, args.gop, gop_seed(g)) for g in my_gops]
+        n_units = world * args.gops_per_gpu
+    G = len(gops)
     frames = torch.from_numpy(np.stack(gops)).to(dev)  # [G, T, 3, Hp, Wp]
     Hp, Wp = frames.shape[-2:]
 
@@ -196,7 +208,7 @@ def main():
     psnr_all = float(np.mean(allst[:, 2]))
 
     pmc_traffic = load_pmc_traffic(args.height, args.width)
-    pframes = args.steps * G * (args.gop - 1) * world
+    pframes = args.steps * n_units * (args.gop - 1)
     value = pframes / dt_max
     nfr = G * (args.gop - 1)
     achieved = x3_flops / (x3_ms * 1e-3) / 1e12 if x3_ms > 0 else 0.0
@@ -216,7 +228,12 @@ def main():
         "config": {"workload": f"DVC P-frame encode+decode with rANS, {args.width}x{args.height} "
                                f"(padded {Wp}x{Hp}) GOP-{args.gop}, lambda=1024 slot",
                    "gops_per_gpu": G, "frames_counted": "P-frames only (I-frame pass-through)",
-                   "parallelism": f"gop-shard x{world}"},
+                   "parallelism": f"gop-shard x{world}"} if args.views <= 0 else
+                  {"workload": f"{args.views}-view DVC P-frame encode+decode with rANS, {args.width}x{args.height} "
+                               f"(padded {Wp}x{Hp}) GOP-{args.gop} per view, lambda=1024 slot",
+                   "views": args.views, "views_per_gpu": G,
+                   "frames_counted": "P-frames only (I-frame pass-through)",
+                   "parallelism": f"view-shard x{world}"},
         "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": F16_MFMA_PEAK_TFLOPS,
                      "unit": "TFLOP/s", "frac": round(achieved / F16_MFMA_PEAK_TFLOPS, 4),
                      "traffic": pmc_traffic.get("hbm_bytes_per_launch"),
@@ -241,8 +258,8 @@ def main():
                             "ms_per_pframe": round(ms / nfr, 3), "gb_per_pframe": round(b / nfr / 1e9, 3),
                             "launches": n}
                         for k, (n, ms, b) in sorted(hbm.items(), key=lambda kv: -kv[1][1])},
-        "quality": {"decoder_bitexact": bitexact_all, "bytes_per_pframe": round(bytes_all / (G * (args.gop - 1) * world), 1),
-                    "bpp_actual": round(bytes_all * 8 / (G * (args.gop - 1) * world * Hp * Wp), 5),
+        "quality": {"decoder_bitexact": bitexact_all, "bytes_per_pframe": round(bytes_all / (n_units * (args.gop - 1)), 1),
+                    "bpp_actual": round(bytes_all * 8 / (n_units * (args.gop - 1) * Hp * Wp), 5),
                     "psnr_db_mean": round(psnr_all, 4),
                     "x3_operand_overflow": x3_overflow},
         "model_tflop_per_pframe": ENC_TFLOP_PER_PFRAME + DEC_TFLOP_PER_PFRAME,

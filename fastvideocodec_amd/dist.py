@@ -19,6 +19,12 @@ def shard_gops(n_gops: int, rank: int, world: int):
     return [g for g in range(n_gops) if g % world == rank]
 
 
+def shard_views(n_views: int, rank: int, world: int):
+    """Camera view v goes to rank v % world (BASELINE configs[4]: 8 views, one per GPU). DVC codes
+    each view as an independent stream; the reference's cross-view MCVC coupling is out of scope."""
+    return [v for v in range(n_views) if v % world == rank]
+
+
 def _dev(device):
     return torch.device(device) if device is not None else torch.device("cpu")
 

@@ -62,3 +62,11 @@ def test_single_process_fallbacks():
     assert fd.max_over_ranks(3.5) == 3.5
     assert fd.gather_bytes(b"abc") == [b"abc"]
     assert fd.gather_stats([1.0, 2.0]).shape == (1, 2)
+
+
+def test_view_sharding_one_view_per_gpu():
+    # BASELINE configs[4]: 8 views on 8 GPUs -> exactly one view per rank, every view once
+    shards = [fd.shard_views(8, r, 8) for r in range(8)]
+    assert shards == [[r] for r in range(8)]
+    shards4 = [fd.shard_views(8, r, 4) for r in range(4)]
+    assert sorted(v for s in shards4 for v in s) == list(range(8)) and all(len(s) == 2 for s in shards4)
