@@ -1,7 +1,7 @@
 #!/bin/bash
 # Row-structured upsample-add / avgpool kernels: parity suite, then two default bench lines.
 export TMPDIR=/tmp
-O=gpurun_out/rows
+O=gpurun_out/${1:-rows}
 mkdir -p $O
 timeout -k 10 400 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread \
   > $O/pytest_gpu.log 2>&1 || { tail -30 $O/pytest_gpu.log; exit 1; }
