@@ -261,7 +261,9 @@ def main():
         "quality": {"decoder_bitexact": bitexact_all, "bytes_per_pframe": round(bytes_all / (n_units * (args.gop - 1)), 1),
                     "bpp_actual": round(bytes_all * 8 / (n_units * (args.gop - 1) * Hp * Wp), 5),
                     "psnr_db_mean": round(psnr_all, 4),
-                    "x3_operand_overflow": x3_overflow},
+                    "x3_operand_overflow": x3_overflow,
+                    "note": "seeded (untrained) codec weights + synthetic GOP: PSNR/bpp are not rate-distortion "
+                            "figures; they are the same arithmetic as the oracle (parity in tests/)"},
         "model_tflop_per_pframe": ENC_TFLOP_PER_PFRAME + DEC_TFLOP_PER_PFRAME,
     }
     result["effective_tflops"] = round(value / world * (ENC_TFLOP_PER_PFRAME + DEC_TFLOP_PER_PFRAME), 2)
