@@ -135,6 +135,24 @@ def test_compress_decompress_bitexact(model, dev):
     assert torch.equal(out[0], rec_enc)
 
 
+def test_compress_deterministic_and_portable(model, dev):
+    """Determinism check (SURVEY §5 race detection): encoding the same frame twice gives the same
+    bytes, and a separately constructed decoder instance reproduces the encoder's recon."""
+    g = np.load(os.path.join(GOLD, "dvc_128x192.npz"))
+    cur = torch.from_numpy(g["input_image"]).to(dev)
+    ref = torch.from_numpy(g["referframe"]).to(dev)
+    bs1, rec1 = model.compress(cur, ref)
+    bs2, rec2 = model.compress(cur, ref)
+    torch.cuda.synchronize()
+    assert torch.equal(rec1, rec2)
+    for part in ("z", "mv", "feature"):
+        assert getattr(bs1, part).to_bytes_list() == getattr(bs2, part).to_bytes_list(), part
+    other = get_codec_model("DVC-pretrained", compression_level=2, device=dev)
+    rec_dec = other.decompress(bs1, ref)
+    torch.cuda.synchronize()
+    assert torch.equal(rec_dec, rec1)
+
+
 def test_compress_streams_vs_oracle_coder(model, dev):
     """Device bitstream == C oracle coder fed the same symbols/indexes/tables."""
     from oracle import coder_ref as R
