@@ -1,12 +1,14 @@
 """1080p DVC P-frame encode+decode throughput on MI355X (BASELINE.json metric, configs[2]).
 
 A step = G GOP-12s per GPU batched along dim 0 (G = --gops-per-gpu, default 4; default 2 timed
-steps = 8 GOPs per run), one GOP per batch slot, at 1920x1080 (replicate-padded to 1920x1088): frame 0 is
-the I-frame (passed through; BPG is out of scope), frames 1..11 are DVC P-frames, each
-encoded (full forward incl. reconstruction + bpp path + rANS range coding into a bitstream)
-and decoded (rANS decode -> hyperprior -> MV synthesis -> motion compensation -> residual
-synthesis) against the previous decoded frame. value = decoded P-frames per second over all
-ranks (I-frames are not counted). Inputs are resident in HBM before the timed region.
+steps = 8 GOPs per run), one GOP per batch slot, at 1920x1080
+(replicate-padded to 1920x1088): frame 0 is the I-frame (passed through; BPG is out of scope),
+frames 1..11 are DVC P-frames, each encoded (full encoder forward incl. its reconstruction, then
+rANS range coding of mv / z / feature into a bitstream) and decoded (rANS decode -> hyperprior ->
+MV synthesis -> motion compensation -> residual synthesis) against the previous decoded frame.
+The bits-estimate kernels of forward() are not in the step: the real bitstream replaces the
+estimate. value = decoded P-frames per second over all ranks (I-frames are not counted). Inputs
+are resident in HBM before the timed region.
 
 Consecutive steps are pipelined the way a streaming encoder runs: a GOP's coder/decoder tail
 (the last frames' latency-bound rANS decode + reconstruction) overlaps the next GOP's encoder
@@ -14,13 +16,20 @@ Consecutive steps are pipelined the way a streaming encoder runs: a GOP's coder/
 all K GOPs is inside the timed region.
 
 Multi-GPU: one process per GPU (torchrun), GOPs sharded by rank, no data-path collective;
-RCCL is used only after timing (max-time all_reduce, metric/bitstream-size all_gather).
+RCCL is used only after timing (max-time all_reduce, per-rank stats all_gather, bitstreams
+gathered to rank 0).
+
+The CPU leg (rank 0, N=1; --cpu-baseline quick|full|none) times the oracle on the host cores and
+reports BASELINE.md §3's parity block from the same frame: symbol / index mismatch counts,
+dPSNR, dbpp_est and a byte-exact stream check against the C oracle coder.
 """
 from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
+import statistics
 import sys
 import time
 
@@ -32,188 +41,282 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 from fastvideocodec_amd import dist as fdist  # noqa: E402
-from fastvideocodec_amd import profiling  # noqa: E402
-from fastvideocodec_amd.gop import encode_decode_gop  # noqa: E402
-from fastvideocodec_amd.models import get_codec_model  # noqa: E402
-from fastvideocodec_amd.synthetic import gop_seed, make_gop  # noqa: E402
 
 HBM_PEAK_BPS = 8.0e12           # MI355X_MICROARCH.md: HBM3E peak (spec; ~6.3 TB/s achievable)
 F16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16/F16 dense matrix peak (~2.5 PF)
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 matrix (v_mfma_f32_32x32x2_f32), dense
-ENC_TFLOP_PER_PFRAME = 2.931   # SURVEY.md §8(d) algorithmic, 1920x1088
-DEC_TFLOP_PER_PFRAME = 1.295
+# SURVEY.md §8(d) algorithmic work at 1920x1088; every layer scales with the frame area
+ENC_TFLOP_1088 = 2.931
+DEC_TFLOP_1088 = 1.295
+AREA_1088 = 1920 * 1088
+METRIC_1080 = "1080p frames/sec encode+decode at λ=1024; bpp/PSNR parity vs CPU ref"
 
 
-def cpu_baseline(H, W, frames_np):
-    """Oracle (CPU PyTorch restatement of the reference forward, validated against the reference's
-    golden fixtures) + C oracle coder, one 1080p P-frame encode+decode on the host cores."""
+def tflop_per_pframe(hp, wp):
+    s = hp * wp / AREA_1088
+    return ENC_TFLOP_1088 * s, DEC_TFLOP_1088 * s
+
+
+def metric_name(height, width):
+    if (height, width) == (1080, 1920):
+        return METRIC_1080
+    return f"{width}x{height} frames/sec encode+decode at λ=1024; bpp/PSNR parity vs CPU ref"
+
+
+# ------------------------------------------------------------------ CPU leg (rank 0, N=1)
+def cpu_cores():
+    """Host cores this process may use: the affinity mask, capped by the cgroup CPU quota (a GPU
+    box shows the whole machine's CPUs in the mask but grants a share of them)."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, math.ceil(int(q) / int(per))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def _median_time(fn, reps):
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        fn()
+        ts.append(time.perf_counter() - t0)
+    return statistics.median(ts), ts
+
+
+def cpu_baseline(model, dev, frames_np, mode="quick"):
+    """The oracle (CPU PyTorch restatement of the reference forward, pinned to the reference's
+    golden fixtures) + the C oracle coder on the host cores, and the parity block of the same
+    frame (GOP 0, frame 1 coded against frame 0, which the GPU run also codes first).
+
+    quick (default, ~30 s of CPU work): 1080p encode+decode once at all cores (the parity sample),
+    256x256 forward median of 3 after a warm-up at all cores and at 1 thread, C coder on one core.
+    full: additionally a warm-up and a median of 3 at 1080p, and 1080p at 1 thread."""
     from oracle import coder_ref as R
     from oracle import dvc_ref
+    from fastvideocodec_amd.synthetic import make_gop
     from fastvideocodec_amd.weights import seeded_torch_state_dict
-    from fastvideocodec_amd import entropy_models as EM
 
-    cores = min(16, len(os.sched_getaffinity(0)))
+    cores = cpu_cores()
     torch.set_num_threads(cores)
     sd = seeded_torch_state_dict()
     cur = torch.from_numpy(frames_np[1:2].copy())
     ref = torch.from_numpy(frames_np[0:1].copy())
-    lt = EM.LaplaceTables()
-    t0 = time.perf_counter()
-    (clipped, *_), inter = dvc_ref.forward(sd, cur, ref, return_intermediates=True)
-    sig = inter["recon_sigma"].numpy()
-    feat = inter["compressed_feature"].numpy().astype(np.int32)
-    idx = R.build_indexes(sig, lt.scale_table)
-    nbytes = 0
-    for c in range(feat.shape[1]):
-        nbytes += len(R.CRef.encode(feat[0, c].ravel(), idx[0, c].ravel(), lt.cdf, lt.cdf_length, lt.offset))
-    dvc_ref.decode(sd, ref, inter["quant_mv"], inter["compressed_z"], inter["compressed_feature"])
-    dt = time.perf_counter() - t0
-    # SURVEY §8(d): also one thread on config 1's 256x256 pair (oracle forward only)
-    from fastvideocodec_amd.synthetic import make_gop
+    Hp, Wp = cur.shape[-2:]
+    state = {}
+
+    def enc_dec():
+        out, inter = dvc_ref.forward(sd, cur, ref, return_intermediates=True)
+        dvc_ref.decode(sd, ref, inter["quant_mv"], inter["compressed_z"], inter["compressed_feature"])
+        state["out"], state["inter"] = out, inter
+
+    full = mode == "full"
+    if full:
+        enc_dec()  # warm-up
+    t_1080, runs_1080 = _median_time(enc_dec, 3 if full else 1)
+    one_thread_1080 = None
+    if full:
+        torch.set_num_threads(1)
+        one_thread_1080 = _median_time(enc_dec, 1)[0]
+        torch.set_num_threads(cores)
+
     small = make_gop(256, 256, 2, 20261015)
-    torch.set_num_threads(1)
     c1, r1 = torch.from_numpy(small[1:2].copy()), torch.from_numpy(small[0:1].copy())
-    dvc_ref.forward(sd, c1, r1)  # warm
-    t1 = time.perf_counter()
-    dvc_ref.forward(sd, c1, r1)
-    dt1 = time.perf_counter() - t1
+    f256 = lambda: dvc_ref.forward(sd, c1, r1)
+    f256()
+    t_256 = _median_time(f256, 3)[0]
+    torch.set_num_threads(1)
+    f256()
+    t_256_1 = _median_time(f256, 3)[0]
     torch.set_num_threads(cores)
+
+    parity, coder = parity_block(model, dev, cur, ref, state["out"], state["inter"], R)
     cpu_model = ""
     try:
         cpu_model = next(l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name"))
     except (OSError, StopIteration):
         pass
-    return {"value": round(1.0 / dt, 4), "unit": "P-frames/s", "cores": cores, "kind": "port",
-            "cpu": cpu_model, "one_thread_256x256_forward_s": round(dt1, 3),
-            "sample": f"1 P-frame {W}x{H}: oracle forward (encode+recon) + oracle decode + C rANS of the "
-                      f"feature latent, torch CPU fp32, {dt:.1f} s",
-            "seconds": round(dt, 2)}
+    res = {"value": round(1.0 / t_1080, 4), "unit": "P-frames/s", "cores": cores, "kind": "port",
+           "cpu": cpu_model, "mode": mode,
+           "sample": f"1 P-frame {Wp}x{Hp} (GOP 0 frame 1): oracle forward (encode + reconstruction) + oracle "
+                     f"decode, torch CPU fp32 on {cores} threads, {'median of 3 after a warm-up' if full else 'one run'}"
+                     f" = {t_1080:.2f} s",
+           "seconds_1080": round(t_1080, 3), "runs_1080": [round(x, 3) for x in runs_1080],
+           "forward_256x256_s": {"threads": cores, "median_of_3": round(t_256, 4)},
+           "forward_256x256_1thread_s": round(t_256_1, 4),
+           "coder_1core": coder}
+    if one_thread_1080 is not None:
+        res["seconds_1080_1thread"] = round(one_thread_1080, 2)
+    return res, parity
 
 
-def load_pmc_traffic(H, W):
-    """HBM bytes per conv_x3_kernel launch from the committed rocprofv3 FETCH_SIZE/WRITE_SIZE passes
-    over `bench.py --serial` (profiles/r1/x3_traffic.json, written by scripts/rocprof_summary.py;
-    FETCH_SIZE doubled per MI355X_MICROARCH.md's gfx950 correction). PMC passes serialise every
-    dispatch and cannot run inside the timed region, so the figure is the profiled one."""
-    path = os.path.join(REPO, "profiles", "r1", "x3_traffic.json")
-    try:
-        with open(path) as f:
-            d = json.load(f)
-    except (OSError, ValueError):
-        return {}
-    if d.get("height") != H or d.get("width") != W:
-        return {}
-    return {"hbm_bytes_per_launch": d.get("hbm_bytes_per_launch"),
-            "source": f"profiles/r1/x3_traffic.json (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, "
-                      f"{d.get('launches')} launches)"}
+def parity_block(model, dev, cur, ref, oracle_out, inter, R):
+    """BASELINE.md §3 parity of the GPU path against the oracle on one frame: symbol and index
+    mismatch counts per latent, dPSNR, dbpp_est, and every device stream vs the C oracle coder
+    (T1: same symbols / indexes / tables -> same bytes; T3: streams of the oracle's own symbols
+    that come out byte-identical). Also times the C coder on one core (symbols/s)."""
+    from fastvideocodec_amd import kernels as K
+
+    with torch.no_grad():
+        out = model(cur.to(dev), ref.to(dev))
+        t = model._encode_graph(cur.to(dev), ref.to(dev))
+        bs = model.compress_tensors(t)
+    c = model._coders
+    tz, tmv, tf = c["tables"]
+    tabs = {"mv": tmv, "z": tz, "feature": tf}
+    keys = {"mv": ("mvfeature", "quant_mv", 128), "z": ("z", "compressed_z", 64),
+            "feature": ("feature", "compressed_feature", 96)}
+    st = c["scale_table"].cpu().numpy()
+    par = {"frame": "GOP 0 frame 1 vs frame 0", "latents": {}}
+    total_sym = total_flip = 0
+    t_enc = t_dec = 0.0
+    nsym = 0
+    for name, (key, gkey, C) in keys.items():
+        gsym = K.latent_to_symbols(t[key], C).cpu().numpy().reshape(C, -1)
+        osym = inter[gkey].numpy().reshape(C, -1).astype(np.int32)
+        if name == "feature":
+            gidx = K.build_indexes(t["sigma"], c["scale_table"], C).cpu().numpy().reshape(C, -1)
+            oidx = R.build_indexes(inter["recon_sigma"].numpy().reshape(C, -1), st)
+        else:
+            gidx = oidx = np.repeat(np.arange(C, dtype=np.int32)[:, None], gsym.shape[1], 1)
+        tb = tabs[name]
+        strings = getattr(bs, name).to_bytes_list()
+        t1_equal = oracle_equal = 0
+        for ch in range(C):
+            t0 = time.perf_counter()
+            s_gpu_syms = R.CRef.encode(gsym[ch], gidx[ch], tb.cdf, tb.cdf_length, tb.offset)
+            t_enc += time.perf_counter() - t0
+            t0 = time.perf_counter()
+            R.CRef.decode(s_gpu_syms, gidx[ch], tb.cdf, tb.cdf_length, tb.offset)
+            t_dec += time.perf_counter() - t0
+            nsym += gsym.shape[1]
+            t1_equal += strings[ch] == s_gpu_syms
+            oracle_equal += strings[ch] == R.CRef.encode(osym[ch], oidx[ch], tb.cdf, tb.cdf_length, tb.offset)
+        flips = int((gsym != osym).sum())
+        total_flip += flips
+        total_sym += gsym.size
+        par["latents"][name] = {"symbols": int(gsym.size), "symbol_mismatches": flips,
+                                "index_mismatches": int((gidx != oidx).sum()), "streams": C,
+                                "streams_bytes_equal_c_oracle_same_symbols": int(t1_equal),
+                                "streams_bytes_equal_c_oracle_on_oracle_symbols": int(oracle_equal)}
+    npx = cur.shape[-1] * cur.shape[-2]
+    psnr_gpu = 10 * math.log10(1.0 / float(out[1]))
+    psnr_cpu = 10 * math.log10(1.0 / float(oracle_out[1]))
+    par.update({
+        "symbol_mismatch_rate": total_flip / total_sym,
+        "symbol_mismatch_bound": 1.56e-5,
+        "dpsnr_db": abs(psnr_gpu - psnr_cpu), "dpsnr_bound_db": 1e-4,
+        "psnr_gpu_db": round(psnr_gpu, 6), "psnr_cpu_db": round(psnr_cpu, 6),
+        "bpp_est_gpu": float(out[7]), "bpp_est_cpu": float(oracle_out[7]),
+        "dbpp_est_rel": abs(float(out[7]) - float(oracle_out[7])) / float(oracle_out[7]),
+        "bpp_actual_gpu": bs.nbytes() * 8 / npx,
+        "bitstream_t1_byte_exact": all(v["streams_bytes_equal_c_oracle_same_symbols"] == v["streams"]
+                                      for v in par["latents"].values()),
+    })
+    coder = {"encode_symbols_per_s": round(nsym / t_enc), "decode_symbols_per_s": round(nsym / t_dec),
+             "symbols": nsym, "note": "oracle/rans_ref.c (-O2), all 288 channel streams of the frame, one core"}
+    return par, coder
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=2)
-    ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--height", type=int, default=1080)
-    ap.add_argument("--width", type=int, default=1920)
-    ap.add_argument("--gop", type=int, default=12)
-    ap.add_argument("--gops-per-gpu", type=int, default=4,
-                    help="GOPs batched per rank per step (SURVEY §8(e)); default 4 x 2 steps = 8 GOPs per run "
-                         "(§8(d)). Measured on MI355X: 1 -> 44.5, 2 -> 47.6, 4 -> 49.1 P-frames/s")
-    ap.add_argument("--views", type=int, default=0,
-                    help="BASELINE configs[4]: V camera views, one GOP stream each, view v -> rank v %% world "
-                         "(replaces --gops-per-gpu; the reference's MCVC couples views, DVC views are independent)")
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--json-out", default=None)
-    ap.add_argument("--breakdown", action="store_true", help="print per-conv-geometry timing to stderr")
-    ap.add_argument("--serial", action="store_true",
-                    help="one HIP stream (no encode/code/decode overlap): per-kernel durations are unshared")
-    args = ap.parse_args()
+# ------------------------------------------------------------------ per-rank workload
+class GpuGopJob:
+    """One rank's share of the benchmark: G GOPs resident in HBM, pipelined encode+decode."""
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+    def __init__(self, args, rank, world, dev):
+        from fastvideocodec_amd.models import get_codec_model
+        from fastvideocodec_amd.synthetic import gop_seed, make_gop
+        self.args, self.dev = args, dev
+        self.model = get_codec_model("DVC-pretrained", compression_level=2, device=dev)
+        self.model.update()
+        if args.views > 0:
+            if args.views < world:
+                raise SystemExit(f"--views {args.views} < world size {world}: a rank would have no view")
+            mine = fdist.shard_views(args.views, rank, world)
+            gops = [make_gop(args.height, args.width, args.gop, gop_seed(0, v)) for v in mine]
+        else:
+            mine = fdist.shard_gops(world * args.gops_per_gpu, rank, world)  # GOP g -> rank g % world
+            gops = [make_gop(args.height, args.width, args.gop, gop_seed(g)) for g in mine]
+        self.gops_np = gops
+        self.units = len(gops)
+        self.frames = torch.from_numpy(np.stack(gops)).to(dev)  # [G, T, 3, Hp, Wp]
+        self.Hp, self.Wp = self.frames.shape[-2:]
 
-    model = get_codec_model("DVC-pretrained", compression_level=2, device=dev)
-    model.update()
-    if args.views > 0:
-        # configs[4]: one GOP stream per camera view, view v -> rank v % world (SURVEY §8(e))
-        if args.views < world:
-            raise SystemExit(f"--views {args.views} < world size {world}: a rank would have no view")
-        my_views = fdist.shard_views(args.views, rank, world)
-        gops = [make_gop(args.height, args.width, args.gop, gop_seed(0, v)) for v in my_views]
-        n_units = args.views
-    else:
-        my_gops = fdist.shard_gops(world * args.gops_per_gpu, rank, world)  # GOP g -> rank g % world
-        gops = [make_gop(args.height, args.width, args.gop, gop_seed(g)) for g in my_gops]
-        n_units = world * args.gops_per_gpu
-    G = len(gops)
-    frames = torch.from_numpy(np.stack(gops)).to(dev)  # [G, T, 3, Hp, Wp]
-    Hp, Wp = frames.shape[-2:]
+    def step(self):
+        from fastvideocodec_amd.gop import encode_decode_gop
+        encode_decode_gop(self.model, self.frames, overlap=not self.args.serial, join=False)
 
-    overlap = not args.serial
+    def sync(self):
+        torch.cuda.synchronize()
+
+    def after_timing(self):
+        """Roofline pass: one serial GOP (single stream) with HIP events around every launch on
+        the launching stream (in the overlapped timed region concurrent kernels would be charged
+        to each other's event windows); plus the streamed GOPs' overflow probes."""
+        from fastvideocodec_amd import gop, profiling
+        from fastvideocodec_amd.gop import encode_decode_gop
+        gop.check_overflow(self.model)  # raises if a timed GOP left the split-precision range
+        timer = profiling.KernelTimer()
+        with timer:
+            encode_decode_gop(self.model, self.frames, overlap=False)
+        r = {"conv": timer.collect(), "x3": timer.collect(x3=True), "x3_bytes": timer.collect_bytes(x3=True),
+             "hbm": timer.collect_hbm()}
+        if self.args.breakdown:
+            for k, (n, ms, fl) in sorted(timer.breakdown().items(), key=lambda kv: -kv[1][1]):
+                print(f"{k:40s} n={n:5d} ms={ms:9.2f} TF/s={fl / (ms * 1e-3) / 1e12:7.2f}", file=sys.stderr)
+        return r
+
+    def verify(self):
+        from fastvideocodec_amd.gop import encode_decode_gop
+        overflow_before = getattr(self.model, "overflow_events", 0)
+        bss, decoded, sses, encs = encode_decode_gop(self.model, self.frames, check=True,
+                                                     overlap=not self.args.serial)
+        torch.cuda.synchronize()
+        npx = self.units * 3 * self.Hp * self.Wp
+        psnrs = [float(10 * np.log10(1.0 / (float(s[0]) / npx))) for s in sses]
+        payload = b"".join(s for bs in bss for s in bs.mv.to_bytes_list() + bs.z.to_bytes_list()
+                           + bs.feature.to_bytes_list())
+        return {"bitexact": all(torch.equal(a, b) for a, b in zip(decoded, encs)),
+                "nbytes": sum(b.nbytes() for b in bss), "psnr": float(np.mean(psnrs)), "payload": payload,
+                "overflow_recomputes": getattr(self.model, "overflow_events", 0) - overflow_before}
+
+
+def run_rank(job, args, rank, world, device):
+    """Warm-up, the timed region (barrier + device sync on both sides, max over ranks), then one
+    collective round after timing. Returns the result dict on rank 0, None elsewhere."""
     for _ in range(args.warmup):
-        encode_decode_gop(model, frames, overlap=overlap, join=False)
-    torch.cuda.synchronize()
+        job.step()
+    job.sync()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    job.sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        encode_decode_gop(model, frames, overlap=overlap, join=False)
-    torch.cuda.synchronize()
+        job.step()
+    job.sync()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    job.sync()
     dt = time.perf_counter() - t0
 
-    # ---- roofline pass: one serial GOP (single stream) with HIP events around every conv launch
-    # on the launching stream; in the overlapped timed region concurrent kernels would be charged
-    # to each other's event windows.
-    timer = profiling.KernelTimer()
-    with timer:
-        encode_decode_gop(model, frames, overlap=False)
-    conv_ms, conv_flops, n_launch = timer.collect()
-    x3_ms, x3_flops, x3_launch = timer.collect(x3=True)
-    x3_bytes = timer.collect_bytes(x3=True)
-    hbm = timer.collect_hbm()
-    if args.breakdown and rank == 0:
-        agg = timer.breakdown()
-        for k, (n, ms, fl) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
-            print(f"{k:40s} n={n:5d} ms={ms:9.2f} TF/s={fl / (ms * 1e-3) / 1e12:7.2f}", file=sys.stderr)
-
-    # ---- verification + quality, outside the timed region
-    from fastvideocodec_amd import kernels as K
-    K.x3_overflow(reset=True)
-    bss, decoded, sses, encs = encode_decode_gop(model, frames, check=True, overlap=overlap)
-    torch.cuda.synchronize()
-    x3_overflow = K.x3_overflow(reset=True)
-    bitexact = all(torch.equal(a, b) for a, b in zip(decoded, encs))
-    nbytes = sum(b.nbytes() for b in bss)
-    npx = G * 3 * Hp * Wp
-    psnrs = [float(10 * np.log10(1.0 / (float(s[0]) / npx))) for s in sses]
-
-    # one collective round after timing (RCCL over xGMI on the GPU box): max time, per-rank
-    # stats, and every rank's bitstream bytes of the verification pass gathered (all ranks)
-    dt_max = fdist.max_over_ranks(dt, dev)
-    allst = fdist.gather_stats([1.0 if bitexact else 0.0, float(nbytes), float(np.mean(psnrs))], dev)
-    payload = b"".join(s for bs in bss for s in bs.mv.to_bytes_list() + bs.z.to_bytes_list()
-                       + bs.feature.to_bytes_list())
-    gathered = fdist.gather_bytes(payload, dev)
+    prof = job.after_timing()
+    ver = job.verify()
+    dt_max = fdist.max_over_ranks(dt, device)
+    allst = fdist.gather_stats([1.0 if ver["bitexact"] else 0.0, float(ver["nbytes"]), ver["psnr"],
+                                float(job.units)], device)
+    gathered = fdist.gather_bytes(ver["payload"], device, dst=0)
+    if rank != 0:
+        return None
+    units = int(allst[:, 3].sum())
+    pframes_per_step = units * (args.gop - 1)
+    value = args.steps * pframes_per_step / dt_max
     bitexact_all = bool(np.all(allst[:, 0] == 1.0)) and sum(len(g) for g in gathered) == int(allst[:, 1].sum())
     bytes_all = float(allst[:, 1].sum())
-    psnr_all = float(np.mean(allst[:, 2]))
-
-    pmc_traffic = load_pmc_traffic(args.height, args.width)
-    pframes = args.steps * n_units * (args.gop - 1)
-    value = pframes / dt_max
-    nfr = G * (args.gop - 1)
-    achieved = x3_flops / (x3_ms * 1e-3) / 1e12 if x3_ms > 0 else 0.0
+    enc_tf, dec_tf = tflop_per_pframe(job.Hp, job.Wp)
+    res_label = f"{args.width}x{args.height} (padded {job.Wp}x{job.Hp})"
     result = {
-        "metric": "1080p frames/sec encode+decode at λ=1024; bpp/PSNR parity vs CPU ref",
+        "metric": metric_name(args.height, args.width),
         "value": round(value, 3),
         "unit": "P-frames/s",
         "n_gpus": world,
@@ -225,19 +328,43 @@ def main():
         "vs_baseline": None,
         "dtype": "f32 (convs: fp32 operands split into fp16 hi/lo, f32 accumulate)",
         "data": "synthetic (seeded GOP generator, SURVEY.md §8(d)); seeded weights + pretrained SpyNet",
-        "config": {"workload": f"DVC P-frame encode+decode with rANS, {args.width}x{args.height} "
-                               f"(padded {Wp}x{Hp}) GOP-{args.gop}, lambda=1024 slot",
-                   "gops_per_gpu": G, "frames_counted": "P-frames only (I-frame pass-through)",
-                   "parallelism": f"gop-shard x{world}"} if args.views <= 0 else
-                  {"workload": f"{args.views}-view DVC P-frame encode+decode with rANS, {args.width}x{args.height} "
-                               f"(padded {Wp}x{Hp}) GOP-{args.gop} per view, lambda=1024 slot",
-                   "views": args.views, "views_per_gpu": G,
-                   "frames_counted": "P-frames only (I-frame pass-through)",
-                   "parallelism": f"view-shard x{world}"},
+        "config": ({"workload": f"DVC P-frame encode+decode with rANS, {res_label} GOP-{args.gop}, lambda=1024 slot",
+                    "gops_per_gpu": job.units, "frames_counted": "P-frames only (I-frame pass-through)",
+                    "parallelism": f"gop-shard x{world}"} if args.views <= 0 else
+                   {"workload": f"{args.views}-view DVC P-frame encode+decode with rANS, {res_label} GOP-{args.gop} "
+                                f"per view, lambda=1024 slot",
+                    "views": args.views, "views_per_gpu": job.units,
+                    "frames_counted": "P-frames only (I-frame pass-through)",
+                    "parallelism": f"view-shard x{world}"}),
+        "model_tflop_per_pframe": round(enc_tf + dec_tf, 3),
+        "effective_tflops": round(value / world * (enc_tf + dec_tf), 2),
+        "quality": {"decoder_bitexact": bitexact_all,
+                    "bytes_per_pframe": round(bytes_all / pframes_per_step, 1),
+                    "bpp_actual": round(bytes_all * 8 / (pframes_per_step * job.Hp * job.Wp), 5),
+                    "psnr_db_mean": round(float(np.mean(allst[:, 2])), 4),
+                    "overflow_recomputes": ver["overflow_recomputes"],
+                    "bitstreams_gathered_to_rank0_bytes": sum(len(g) for g in gathered),
+                    "note": "seeded (untrained) codec weights + synthetic GOP: PSNR/bpp are not rate-distortion "
+                            "figures; the coder's symbol statistics (and so its timing) are those of untrained "
+                            "weights (~5 bpp vs DVC's 0.137 bpp at lambda=1024)"},
+    }
+    if prof is not None:
+        result.update(roofline_fields(prof, job, args))
+    return result
+
+
+def roofline_fields(prof, job, args):
+    conv_ms, conv_flops, n_launch = prof["conv"]
+    x3_ms, x3_flops, x3_launch = prof["x3"]
+    x3_bytes = prof["x3_bytes"]
+    nfr = job.units * (args.gop - 1)
+    achieved = x3_flops / (x3_ms * 1e-3) / 1e12 if x3_ms > 0 else 0.0
+    pmc = load_pmc_traffic(args.height, args.width)
+    return {
         "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": F16_MFMA_PEAK_TFLOPS,
                      "unit": "TFLOP/s", "frac": round(achieved / F16_MFMA_PEAK_TFLOPS, 4),
-                     "traffic": pmc_traffic.get("hbm_bytes_per_launch"),
-                     "traffic_source": pmc_traffic.get("source"),
+                     "traffic": pmc.get("hbm_bytes_per_launch"),
+                     "traffic_source": pmc.get("source"),
                      "avg_launch_us": round(x3_ms * 1e3 / x3_launch, 2) if x3_launch else None,
                      "algorithmic_bytes_per_launch": round(x3_bytes / x3_launch) if x3_launch else None,
                      "algorithmic_gbps": round(x3_bytes / (x3_ms * 1e-3) / 1e9, 1) if x3_ms else None,
@@ -257,18 +384,73 @@ def main():
                             "frac_of_8tbps": round(b / (ms * 1e-3) / HBM_PEAK_BPS, 4) if ms else None,
                             "ms_per_pframe": round(ms / nfr, 3), "gb_per_pframe": round(b / nfr / 1e9, 3),
                             "launches": n}
-                        for k, (n, ms, b) in sorted(hbm.items(), key=lambda kv: -kv[1][1])},
-        "quality": {"decoder_bitexact": bitexact_all, "bytes_per_pframe": round(bytes_all / (n_units * (args.gop - 1)), 1),
-                    "bpp_actual": round(bytes_all * 8 / (n_units * (args.gop - 1) * Hp * Wp), 5),
-                    "psnr_db_mean": round(psnr_all, 4),
-                    "x3_operand_overflow": x3_overflow,
-                    "note": "seeded (untrained) codec weights + synthetic GOP: PSNR/bpp are not rate-distortion "
-                            "figures; they are the same arithmetic as the oracle (parity in tests/)"},
-        "model_tflop_per_pframe": ENC_TFLOP_PER_PFRAME + DEC_TFLOP_PER_PFRAME,
+                        for k, (n, ms, b) in sorted(prof["hbm"].items(), key=lambda kv: -kv[1][1])},
     }
-    result["effective_tflops"] = round(value / world * (ENC_TFLOP_PER_PFRAME + DEC_TFLOP_PER_PFRAME), 2)
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(Hp, Wp, gops[0])
+
+
+def load_pmc_traffic(H, W):
+    """HBM bytes per conv_x3_kernel launch from the committed rocprofv3 FETCH_SIZE/WRITE_SIZE passes
+    over `bench.py --serial` (profiles/<round>/x3_traffic.json, written by scripts/rocprof_summary.py;
+    FETCH_SIZE doubled per MI355X_MICROARCH.md's gfx950 correction). PMC passes serialise every
+    dispatch and cannot run inside the timed region, so the figure is the profiled one."""
+    for rnd in ("r2", "r1"):
+        path = os.path.join(REPO, "profiles", rnd, "x3_traffic.json")
+        try:
+            with open(path) as f:
+                d = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if d.get("height") != H or d.get("width") != W:
+            continue
+        return {"hbm_bytes_per_launch": d.get("hbm_bytes_per_launch"),
+                "source": f"profiles/{rnd}/x3_traffic.json (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, "
+                          f"{d.get('launches')} launches)"}
+    return {}
+
+
+def parse_args(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--gop", type=int, default=12)
+    ap.add_argument("--gops-per-gpu", type=int, default=4,
+                    help="GOPs batched per rank per step (SURVEY §8(e)); default 4 x 2 steps = 8 GOPs per run "
+                         "(§8(d)). Measured on MI355X: 1 -> 44.5, 2 -> 47.6, 4 -> 49.1 P-frames/s")
+    ap.add_argument("--views", type=int, default=0,
+                    help="BASELINE configs[4]: V camera views, one GOP stream each, view v -> rank v %% world "
+                         "(replaces --gops-per-gpu; the reference's MCVC couples views, DVC views are independent)")
+    ap.add_argument("--cpu-baseline", choices=("quick", "full", "none"), default="quick",
+                    help="CPU leg + parity block on rank 0 at N=1: quick (~30 s), full (BASELINE.md §3 protocol, "
+                         "several minutes), none")
+    ap.add_argument("--no-cpu-baseline", action="store_true", help="same as --cpu-baseline none")
+    ap.add_argument("--json-out", default=None)
+    ap.add_argument("--breakdown", action="store_true", help="print per-conv-geometry timing to stderr")
+    ap.add_argument("--serial", action="store_true",
+                    help="one HIP stream (no encode/code/decode overlap): per-kernel durations are unshared")
+    args = ap.parse_args(argv)
+    if args.no_cpu_baseline:
+        args.cpu_baseline = "none"
+    return args
+
+
+def main(argv=None):
+    args = parse_args(argv)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    job = GpuGopJob(args, rank, world, dev)
+    result = run_rank(job, args, rank, world, dev)
+    if rank == 0 and world == 1 and args.cpu_baseline != "none":
+        cb, parity = cpu_baseline(job.model, dev, job.gops_np[0], args.cpu_baseline)
+        result["cpu_baseline"] = cb
+        result["quality"]["parity"] = parity
     if rank == 0:
         line = json.dumps(result)
         print(line, flush=True)

@@ -27,10 +27,8 @@ _SIGS = {
     "fvc_conv_x3_supported": (c_int, [c_int] * 5),
     "fvc_conv_x3_wpack_bytes": (c_size_t, [c_int] * 5),
     "fvc_conv_x3_pack_weight": (c_int, [vp, vp, vp] + [c_int] * 5),
-    "fvc_conv2d_nhwc_x3": (c_int, [vp, vp, c_float, vp, vp, vp] + [c_int] * 10 + [vp]),
-    "fvc_deconv2d_nhwc_x3": (c_int, [vp, vp, c_float, vp, vp, vp] + [c_int] * 10 + [vp]),
-    "fvc_x3_set_cu_reserve": (c_int, [c_int]),
-    "fvc_x3_overflow_flag": (c_int, [vp, c_int]),
+    "fvc_conv2d_nhwc_x3": (c_int, [vp, vp, c_float, vp, vp, vp] + [c_int] * 11 + [vp, vp]),
+    "fvc_deconv2d_nhwc_x3": (c_int, [vp, vp, c_float, vp, vp, vp] + [c_int] * 11 + [vp, vp]),
     "fvc_nchw_to_nhwc": (c_int, [vp, vp, c_int, c_int, c_int, c_int, c_int, vp]),
     "fvc_nhwc_to_nchw": (c_int, [vp, vp, c_int, c_int, c_int, c_int, c_int, c_int, vp]),
     "fvc_avgpool2_nhwc": (c_int, [vp, vp, c_int, c_int, c_int, c_int, vp]),
@@ -50,12 +48,15 @@ _SIGS = {
     "fvc_symbols_to_latent": (c_int, [vp, vp] + [c_int] * 5 + [vp]),
     "fvc_build_indexes": (c_int, [vp, vp, c_int, vp] + [c_int] * 5 + [vp]),
     "fvc_channel_indexes": (c_int, [vp, c_int, c_int, c_int, vp]),
+    "fvc_quantize_symbols": (c_int, [vp, vp, vp, c_size_t, vp]),
+    "fvc_dequantize_symbols": (c_int, [vp, vp, vp, c_size_t, vp]),
+    "fvc_build_indexes_flat": (c_int, [vp, vp, c_int, vp, c_size_t, vp]),
     "fvc_pmf_to_quantized_cdf": (c_int, [vp, c_int, c_int, vp]),
     "fvc_rans_encode_ws_bytes": (c_size_t, [ctypes.c_int64]),
     "fvc_rans_encode": (c_int, [vp, vp, vp, c_int, ctypes.c_int64, vp, c_int, vp, vp, vp, vp, vp, vp, vp]),
     "fvc_rans_lut_bytes": (c_size_t, [c_int, c_int]),
     "fvc_rans_build_lut": (c_int, [vp, c_int, vp, c_int, vp, vp]),
-    "fvc_rans_pack": (c_int, [vp, vp, vp, c_int, vp, vp, vp]),
+    "fvc_rans_pack": (c_int, [vp, vp, vp, c_int, vp, vp, vp, vp]),
     "fvc_rans_decode": (c_int, [vp, vp, vp, vp, c_int, c_int, c_int, vp, vp, vp, vp, vp, vp]),
 }
 

@@ -60,6 +60,30 @@ __global__ void k_channel_indexes(int32_t* __restrict__ idx, int B, int HW, int 
     idx[e] = (int32_t)((e / HW) % C);
 }
 
+// compressai EntropyModel.quantize(x, "symbols", means) = round(x - means).int() and
+// dequantize(symbols, means) = symbols + means, elementwise over any contiguous layout
+__global__ void k_quantize_symbols(const float* __restrict__ x, const float* __restrict__ means,
+                                   int32_t* __restrict__ sym, size_t n) {
+  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < n; e += (size_t)gridDim.x * blockDim.x)
+    sym[e] = (int32_t)rintf(means ? x[e] - means[e] : x[e]);
+}
+
+__global__ void k_dequantize_symbols(const int32_t* __restrict__ sym, const float* __restrict__ means,
+                                     float* __restrict__ out, size_t n) {
+  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < n; e += (size_t)gridDim.x * blockDim.x)
+    out[e] = means ? (float)sym[e] + means[e] : (float)sym[e];
+}
+
+__global__ void k_build_indexes_flat(const float* __restrict__ scales, const float* __restrict__ table, int nt,
+                                     int32_t* __restrict__ idx, size_t n) {
+  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < n; e += (size_t)gridDim.x * blockDim.x) {
+    const float s = fmaxf(scales[e], 0.11f);
+    int v = nt - 1;
+    for (int k = 0; k < nt - 1; ++k) v -= (s <= table[k]) ? 1 : 0;
+    idx[e] = v;
+  }
+}
+
 // ---- ryg_rans 64-bit primitives (rans64.h) + compressai bypass extension
 __device__ __forceinline__ bool enc_put_bits(uint64_t& x, uint32_t*& ptr, const uint32_t* lo, uint32_t val) {
   const uint32_t freq = 1u << (16 - kBypassPrec);
@@ -198,23 +222,34 @@ __global__ void k_rans_encode(const EncSym* __restrict__ prep, const uint32_t* _
   }
 }
 
-__global__ void k_pack_scan(const int32_t* __restrict__ nwords, int n, int64_t* __restrict__ pack_off) {
-  // single block, fixed-order exclusive scan
+__global__ void k_pack_scan(const int32_t* __restrict__ nwords, int n, int64_t* __restrict__ pack_off,
+                            int32_t* __restrict__ status) {
+  // single block, fixed-order exclusive scan; a stream whose encode ran out of space (nwords < 0)
+  // packs as empty and sets status = FVC_ENOSPC
   __shared__ int64_t part[kBlk];
+  __shared__ int bad[kBlk];
   const int per = (n + kBlk - 1) / kBlk;
   const int b0 = threadIdx.x * per;
   int64_t s = 0;
-  for (int i = b0; i < b0 + per && i < n; ++i) s += nwords[i] > 0 ? nwords[i] : 0;
+  int nbad = 0;
+  for (int i = b0; i < b0 + per && i < n; ++i) {
+    s += nwords[i] > 0 ? nwords[i] : 0;
+    nbad += nwords[i] < 0 ? 1 : 0;
+  }
   part[threadIdx.x] = s;
+  bad[threadIdx.x] = nbad;
   __syncthreads();
   if (threadIdx.x == 0) {
     int64_t run = 0;
+    int any = 0;
     for (int t = 0; t < kBlk; ++t) {
       const int64_t v = part[t];
       part[t] = run;
       run += v;
+      any |= bad[t];
     }
     pack_off[n] = run;
+    if (status) status[0] = any ? FVC_ENOSPC : 0;
   }
   __syncthreads();
   int64_t run = part[threadIdx.x];
@@ -427,6 +462,33 @@ int fvc_channel_indexes(int32_t* idx, int batch, int hw, int c, fvc_stream_t s) 
   return 0;
 }
 
+int fvc_quantize_symbols(const float* x, const float* means, int32_t* sym, size_t n, fvc_stream_t s) {
+  if ((!x || !sym) && n) return FVC_EINVAL;
+  if (!n) return 0;
+  hipLaunchKernelGGL(k_quantize_symbols, dim3(grid_for(n)), dim3(kBlk), 0, (hipStream_t)s, x, means, sym, n);
+  FVC_CHECK_LAUNCH();
+  return 0;
+}
+
+int fvc_dequantize_symbols(const int32_t* sym, const float* means, float* out, size_t n, fvc_stream_t s) {
+  if ((!sym || !out) && n) return FVC_EINVAL;
+  if (!n) return 0;
+  hipLaunchKernelGGL(k_dequantize_symbols, dim3(grid_for(n)), dim3(kBlk), 0, (hipStream_t)s, sym, means, out, n);
+  FVC_CHECK_LAUNCH();
+  return 0;
+}
+
+int fvc_build_indexes_flat(const float* scales, const float* table, int nt, int32_t* idx, size_t n,
+                           fvc_stream_t s) {
+  if ((!scales || !idx) && n) return FVC_EINVAL;
+  if (!table || nt < 1) return FVC_EINVAL;
+  if (!n) return 0;
+  hipLaunchKernelGGL(k_build_indexes_flat, dim3(grid_for(n)), dim3(kBlk), 0, (hipStream_t)s, scales, table, nt,
+                     idx, n);
+  FVC_CHECK_LAUNCH();
+  return 0;
+}
+
 size_t fvc_rans_encode_ws_bytes(int64_t nsymbols) { return (size_t)nsymbols * (sizeof(EncSym) + 4); }
 
 int fvc_rans_encode(const int32_t* symbols, const int32_t* indexes, const int64_t* sym_off, int nstreams,
@@ -468,9 +530,9 @@ int fvc_rans_build_lut(const int32_t* cdfs, int cdf_stride, const int32_t* cdf_s
 }
 
 int fvc_rans_pack(const uint32_t* words, const int64_t* word_off, const int32_t* nwords, int nstreams,
-                  int64_t* pack_off, uint32_t* out, fvc_stream_t s) {
+                  int64_t* pack_off, uint32_t* out, int32_t* status, fvc_stream_t s) {
   if (!words || !word_off || !nwords || !pack_off || !out || nstreams <= 0) return FVC_EINVAL;
-  hipLaunchKernelGGL(k_pack_scan, dim3(1), dim3(kBlk), 0, (hipStream_t)s, nwords, nstreams, pack_off);
+  hipLaunchKernelGGL(k_pack_scan, dim3(1), dim3(kBlk), 0, (hipStream_t)s, nwords, nstreams, pack_off, status);
   FVC_CHECK_LAUNCH();
   hipLaunchKernelGGL(k_pack_copy, dim3(nstreams), dim3(kBlk), 0, (hipStream_t)s, words, word_off, nwords, pack_off,
                      out);

@@ -18,7 +18,8 @@
 // fp32 conv to ~1e-6 relative (tests/test_gpu_kernels.py bounds it like the fp32 kernel).
 // Three fp16 MFMAs (3 x 32 cycles per K=16) replace eight fp32 ones (8 x 64 cycles): 5.3x
 // less matrix time per MAC. An activation with |v| >= 65000 (or NaN) cannot be represented:
-// the staging code raises a device flag (fvc_x3_overflow_flag) instead of silently saturating.
+// the staging code ORs 1 into the caller's device flag (overflow_flag argument) instead of
+// silently saturating; the host layer checks it and recomputes on the fp32 kernels.
 //
 // Tiling: GEMM M = output pixels (32-pixel strips), N = output channels (32-channel N-tiles),
 // K = taps x input channels walked in k8-blocks = (tap, 8 consecutive channels). One MFMA
@@ -68,8 +69,6 @@ constexpr bool kInterleave = false;
 constexpr int kNPL = kSingleAcc ? 3 : 2;   // weight planes per (k-step, N-tile)
 constexpr int kFrag = 64 * kNPL;          // uint4 per (k-step, N-tile)
 
-__device__ int g_x3_overflow;
-
 struct X3Args {
   const float* x;
   const uint4* w;
@@ -92,6 +91,7 @@ struct X3Args {
   int ps;                          // LDS plane stride (halves): 8 x (pixels rounded to 8 mod 16)
   int bq;                          // BL: uint4 per LDS weight buffer (max k-steps x WN x kFrag)
   unsigned y_bytes;                // bytes of y (and res): < 4 GB - 256, the buffer range
+  int* ovf;                        // caller's overflow flag (device int; may be null)
   int toff[4][kMaxTapsX + 1];      // LDS offset (halves) of each tap's window; 0 past ntaps
 };
 
@@ -653,7 +653,7 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(const X3Args a) {
       }
     }
   }
-  if (!(mx < 65000.f)) atomicOr(&g_x3_overflow, 1);
+  if (!(mx < 65000.f) && a.ovf) atomicOr(a.ovf, 1);
 }
 
 // ------------------------------------------------------------------ host-side geometry
@@ -775,8 +775,6 @@ static bool x3_cfg(int cin, int cout, int ks, int stride, int transposed, X3Cfg&
   return true;
 }
 
-static int g_x3_reserve = 0;  // fvc_x3_set_cu_reserve
-
 static int x3_num_cus() {
   static int n = 0;
   if (!n) {
@@ -870,7 +868,7 @@ static int x3_launch_cc(int wm, int wn, int bl, int iop, const X3Args& a, dim3 g
 
 static int run_x3(const float* x, const void* wpack, float osc, const float* bias, const float* res,
                   float* y, int batch, int h, int w, int cin, int cout, int ks, int stride, int transposed,
-                  int in_op, int act, int post_op, hipStream_t s) {
+                  int in_op, int act, int post_op, int cu_reserve, int* ovf, hipStream_t s) {
   X3Cfg c;
   if (!x3_cfg(cin, cout, ks, stride, transposed, c)) return FVC_EINVAL;
   if (!x || !wpack || !bias || !y || batch <= 0 || h <= 0 || w <= 0) return FVC_EINVAL;
@@ -896,12 +894,13 @@ static int run_x3(const float* x, const void* wpack, float osc, const float* bia
     const int b1 = batch / 2;
     const size_t xs = (size_t)h * w * c.cinp, ys = (size_t)a.Ho * a.Wo * a.coutp;
     int rc = run_x3(x, wpack, osc, bias, res, y, b1, h, w, cin, cout, ks, stride, transposed, in_op, act,
-                    post_op, s);
+                    post_op, cu_reserve, ovf, s);
     if (rc) return rc;
     return run_x3(x + b1 * xs, wpack, osc, bias, res ? res + b1 * ys : nullptr, y + b1 * ys, batch - b1, h, w, cin, cout, ks,
-                  stride, transposed, in_op, act, post_op, s);
+                  stride, transposed, in_op, act, post_op, cu_reserve, ovf, s);
   }
   a.y_bytes = (unsigned)ybytes;
+  a.ovf = ovf;
   a.sin = c.sin; a.sout = c.sout; a.nclass = c.nclass; a.nchunks = c.nchunks; a.ntp = c.ntp;
   a.dymin = c.dymin; a.dxmin = c.dxmin;
   a.ir = (c.th - 1) * c.sin + 1 + (c.dymax - c.dymin);
@@ -949,10 +948,10 @@ static int run_x3(const float* x, const void* wpack, float osc, const float* bia
     while (wn > 1 && base * (c.ntp / wn) < 2LL * x3_num_cus()) wn >>= 1;
   // persistent grid: ~one 8-wave block per CU (FVC_X3_BPC blocks per CU), each walking a
   // contiguous run of spatial tiles
-  // FVC_X3_RESERVE CUs are left out of the persistent grid for kernels of other streams (the
+  // cu_reserve CUs are left out of the persistent grid for kernels of other streams (the
   // latency-bound rANS chains): a block that cannot find a free CU would start only when another
-  // block has finished its whole run, doubling the launch's time
-  const int reserve = env_int("FVC_X3_RESERVE", -1) >= 0 ? env_int("FVC_X3_RESERVE", 0) : g_x3_reserve;
+  // block has finished its whole run, doubling the launch's time (FVC_X3_RESERVE overrides)
+  const int reserve = env_int("FVC_X3_RESERVE", -1) >= 0 ? env_int("FVC_X3_RESERVE", 0) : cu_reserve;
   const int ncu = x3_num_cus() - (reserve < x3_num_cus() / 2 ? reserve : x3_num_cus() / 2);
   const long long yz = (long long)(c.ntp / wn) * batch;
   const int bpc = env_int("FVC_X3_BPC", 1);
@@ -1038,36 +1037,20 @@ int fvc_conv_x3_pack_weight(const float* w, void* wp, float* osc_out, int cin, i
 
 int fvc_conv2d_nhwc_x3(const float* x, const void* wpack, float osc, const float* bias,
                        const float* res, float* y, int batch, int h, int w, int cin, int cout,
-                       int ksize, int stride, int in_op, int act, int post_op, fvc_stream_t stream) {
+                       int ksize, int stride, int in_op, int act, int post_op, int cu_reserve,
+                       int* overflow_flag, fvc_stream_t stream) {
+  if (cu_reserve < 0) return FVC_EINVAL;
   return run_x3(x, wpack, osc, bias, res, y, batch, h, w, cin, cout, ksize, stride, 0, in_op, act,
-                post_op, (hipStream_t)stream);
+                post_op, cu_reserve, overflow_flag, (hipStream_t)stream);
 }
 
 int fvc_deconv2d_nhwc_x3(const float* x, const void* wpack, float osc, const float* bias,
                          const float* res, float* y, int batch, int h, int w, int cin, int cout,
-                         int ksize, int stride, int in_op, int act, int post_op,
-                         fvc_stream_t stream) {
+                         int ksize, int stride, int in_op, int act, int post_op, int cu_reserve,
+                         int* overflow_flag, fvc_stream_t stream) {
+  if (cu_reserve < 0) return FVC_EINVAL;
   return run_x3(x, wpack, osc, bias, res, y, batch, h, w, cin, cout, ksize, stride, 1, in_op, act,
-                post_op, (hipStream_t)stream);
-}
-
-int fvc_x3_set_cu_reserve(int ncu) {
-  if (ncu < 0) return FVC_EINVAL;
-  g_x3_reserve = ncu;
-  return 0;
-}
-
-int fvc_x3_overflow_flag(int* host_flag, int reset) {
-  if (!host_flag) return FVC_EINVAL;
-  hipError_t e = hipMemcpyFromSymbol(host_flag, HIP_SYMBOL(g_x3_overflow), sizeof(int), 0,
-                                     hipMemcpyDeviceToHost);
-  if (e != hipSuccess) return -(int)e;
-  if (reset) {
-    const int zero = 0;
-    e = hipMemcpyToSymbol(HIP_SYMBOL(g_x3_overflow), &zero, sizeof(int), 0, hipMemcpyHostToDevice);
-    if (e != hipSuccess) return -(int)e;
-  }
-  return 0;
+                post_op, cu_reserve, overflow_flag, (hipStream_t)stream);
 }
 
 }  // extern "C"

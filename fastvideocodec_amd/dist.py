@@ -3,8 +3,8 @@
 GOPs are independent (each starts from its own I-frame; the only dependency, ``x_prev``, is inside
 a GOP, ``models.py:372-376``), so ranks never exchange data while coding. After coding, one
 collective round moves the small results: the per-rank elapsed time (MAX), per-rank metrics
-(all_gather) and, optionally, every rank's bitstream bytes to rank 0 (all_gather of lengths, then
-all_gather of zero-padded payloads — a few hundred KB per frame, latency-bound on xGMI).
+(all_gather of a few floats) and every rank's bitstream bytes to rank 0 only (gather of lengths,
+then gather of zero-padded payloads — a few hundred KB per frame, latency-bound on xGMI).
 Works with ``nccl`` (RCCL on ROCm; device tensors) and ``gloo`` (CPU tensors, tests).
 """
 from __future__ import annotations
@@ -46,21 +46,28 @@ def gather_stats(stats, device=None):
     return torch.stack(out).cpu().numpy()
 
 
-def gather_bytes(payload: bytes, device=None):
-    """Every rank contributes one byte string; returns the list of all ranks' strings (on every
-    rank). Two collectives: lengths, then zero-padded payloads."""
+def gather_bytes(payload: bytes, device=None, dst: int = 0):
+    """Every rank contributes one byte string; rank ``dst`` gets the list of all ranks' strings,
+    the other ranks get None (the bitstreams go to one writer, not to everyone).
+    Two collectives: a gather of the lengths, then a gather of the zero-padded payloads
+    (torch.distributed.gather: RCCL send/recv under nccl, gloo on CPU)."""
     dev = _dev(device)
     if not (dist.is_initialized() and dist.get_world_size() > 1):
         return [payload]
     world = dist.get_world_size()
+    me = dist.get_rank()
     n = torch.tensor([len(payload)], dtype=torch.int64, device=dev)
-    lens = [torch.zeros_like(n) for _ in range(world)]
-    dist.all_gather(lens, n)
-    lens = [int(x.item()) for x in lens]
-    cap = max(max(lens), 1)
+    lens = [torch.zeros_like(n) for _ in range(world)] if me == dst else None
+    dist.gather(n, lens, dst=dst)
+    # every rank needs the common padded size: one tiny all_reduce(MAX) of the length
+    cap_t = n.clone()
+    dist.all_reduce(cap_t, op=dist.ReduceOp.MAX)
+    cap = max(int(cap_t.item()), 1)
     buf = torch.zeros(cap, dtype=torch.uint8, device=dev)
     if payload:
         buf[: len(payload)] = torch.frombuffer(bytearray(payload), dtype=torch.uint8).to(dev)
-    outs = [torch.zeros_like(buf) for _ in range(world)]
-    dist.all_gather(outs, buf)
-    return [bytes(o[:L].cpu().numpy().tobytes()) for o, L in zip(outs, lens)]
+    outs = [torch.zeros_like(buf) for _ in range(world)] if me == dst else None
+    dist.gather(buf, outs, dst=dst)
+    if me != dst:
+        return None
+    return [bytes(o[: int(L.item())].cpu().numpy().tobytes()) for o, L in zip(outs, lens)]

@@ -144,17 +144,26 @@ class LaplaceTables:
 
 # ------------------------------------------------------------------ device range coder
 class EncodedStreams:
-    """Packed rANS output of S streams: words (uint32 little-endian) + offsets (in words)."""
+    """Packed rANS output of S streams: words (uint32 little-endian) + offsets (in words).
+    ``status`` (device int32[1], from fvc_rans_pack) is FVC_ENOSPC if a stream ran out of space;
+    reading the bytes checks it."""
 
-    def __init__(self, packed: torch.Tensor, pack_off: torch.Tensor, nstreams: int):
+    def __init__(self, packed: torch.Tensor, pack_off: torch.Tensor, nstreams: int, status=None):
         self.packed = packed
         self.pack_off = pack_off
         self.nstreams = nstreams
+        self.status = status
 
     def nbytes_device(self) -> torch.Tensor:
         return self.pack_off[-1] * 4
 
+    def check(self):
+        """Raise FvcError if the encoder reported an error (waits for the encode)."""
+        if self.status is not None and int(self.status.item()) != 0:
+            raise _lib.FvcError(f"rANS encode failed with status {int(self.status.item())}")
+
     def to_bytes_list(self):
+        self.check()
         off = self.pack_off.cpu().numpy()
         words = self.packed[: int(off[-1])].cpu().numpy().view(np.uint32)
         return [words[off[i]: off[i + 1]].astype("<u4").tobytes() for i in range(self.nstreams)]
@@ -210,20 +219,25 @@ class RangeCoder:
         ws = torch.empty(max(1, _lib.load().fvc_rans_encode_ws_bytes(S * n) // 4), dtype=torch.int32,
                          device=self.device)
         st = K.stream_handle()
+        if n == 0:  # every stream is just the flushed initial state; the kernels need real pointers
+            symbols = indexes = torch.zeros(1, dtype=torch.int32, device=self.device)
         _lib.call("fvc_rans_encode", symbols.data_ptr(), indexes.data_ptr(), sym_off.data_ptr(), S, S * n,
                   self.cdf.data_ptr(), self.cdf.shape[1], self.cdf_length.data_ptr(), self.offset.data_ptr(),
                   ws.data_ptr(), words.data_ptr(), word_off.data_ptr(), nwords.data_ptr(), st)
         pack_off = torch.empty(S + 1, dtype=torch.int64, device=self.device)
         packed = torch.empty_like(words)
+        status = torch.empty(1, dtype=torch.int32, device=self.device)
         _lib.call("fvc_rans_pack", words.data_ptr(), word_off.data_ptr(), nwords.data_ptr(), S,
-                  pack_off.data_ptr(), packed.data_ptr(), st)
-        return EncodedStreams(packed, pack_off, S)
+                  pack_off.data_ptr(), packed.data_ptr(), status.data_ptr(), st)
+        return EncodedStreams(packed, pack_off, S, status)
 
     def decode(self, enc: EncodedStreams, indexes: torch.Tensor, check=True) -> torch.Tensor:
         S, n = indexes.shape
         K._chk(indexes, name="indexes", dtype=torch.int32)
         if enc.nstreams != S:
             raise ValueError("stream count mismatch")
+        if check:
+            enc.check()
         sym_off = self._sym_off(S, n)
         out = torch.empty((S, n), dtype=torch.int32, device=self.device)
         status = torch.empty(S, dtype=torch.int32, device=self.device)
@@ -259,9 +273,7 @@ class RansEncoder:
         if idx.size and (idx.min() < 0 or idx.max() >= len(cdfs)):
             raise ValueError("index out of range")
         coder = RangeCoder(cdf, sizes, offs, self.device)
-        n = len(symbols)
-        if n == 0:
-            return b""
+        n = len(symbols)  # n == 0 still flushes the initial state (8 bytes), as compressai does
         sym = torch.tensor(np.asarray(symbols, np.int32).reshape(1, n), device=self.device)
         ind = torch.tensor(idx.astype(np.int32).reshape(1, n), device=self.device)
         return coder.encode(sym, ind).to_bytes_list()[0]
@@ -282,3 +294,215 @@ class RansDecoder:
         ind = torch.tensor(np.asarray(indexes, np.int32).reshape(1, n), device=self.device)
         enc = EncodedStreams.from_bytes_list([bytes(encoded)], self.device)
         return coder.decode(enc, ind).cpu().numpy().reshape(-1).tolist()
+
+
+# ------------------------------------------------------------------ compressai-framed API
+# compressai's EntropyModel.compress emits ONE string per batch item covering the item's whole
+# (C, H, W) latent in C order (entropy_models.py:80-94 -> compressai EntropyModel.compress /
+# decompress). The classes below reproduce that framing and API on the device coder: the B
+# strings of a batch are B independent rANS streams of C*H*W symbols, coded in one launch. (The
+# codec's own bitstream, net.PFrameBitstream, cuts each item into one stream per channel so that
+# decode runs C-way parallel; both framings code the same symbol sequence per stream the way
+# compressai's encode_with_indexes does.)
+class _CompressaiEntropyModel:
+    """compressai.entropy_models.EntropyModel surface: buffers ``_quantized_cdf``,
+    ``_cdf_length``, ``_offset``; ``compress(inputs, indexes, means)`` -> list[bytes];
+    ``decompress(strings, indexes, dtype, means)``. Tensors are NCHW on the device."""
+
+    def __init__(self, device=None):
+        self.device = torch.device(device) if device is not None else torch.device("cuda")
+        self._quantized_cdf = self._cdf_length = self._offset = None
+        self._coder = None
+
+    def _set_tables(self, cdf, cdf_length, offset):
+        self._coder = RangeCoder(cdf, cdf_length, offset, self.device)
+        self._quantized_cdf = self._coder.cdf
+        self._cdf_length = self._coder.cdf_length
+        self._offset = self._coder.offset
+
+    def _check_ready(self):
+        if self._coder is None:
+            raise ValueError("Uninitialized CDFs. Run update() first")
+
+    def quantize_symbols(self, inputs, means=None) -> torch.Tensor:
+        """round(inputs - means).int() (EntropyModel.quantize(..., "symbols", means))."""
+        x = inputs.float().contiguous()
+        K._chk(x, name="inputs")
+        m = None
+        if means is not None:
+            m = means.float().expand_as(x).contiguous()
+            K._chk(m, x.shape, name="means")
+        sym = torch.empty(x.shape, dtype=torch.int32, device=x.device)
+        _lib.call("fvc_quantize_symbols", x.data_ptr(), K._ptr(m), sym.data_ptr(), x.numel(), K.stream_handle())
+        return sym
+
+    def dequantize(self, symbols, means=None, dtype=torch.float):
+        out = torch.empty(symbols.shape, dtype=torch.float32, device=symbols.device)
+        m = None
+        if means is not None:
+            m = means.float().expand(symbols.shape).contiguous()
+        _lib.call("fvc_dequantize_symbols", symbols.data_ptr(), K._ptr(m), out.data_ptr(), symbols.numel(),
+                  K.stream_handle())
+        return out.to(dtype)
+
+    def compress(self, inputs, indexes, means=None):
+        self._check_ready()
+        if inputs.dim() < 2:
+            raise ValueError("Invalid `inputs` size. Expected a tensor with at least 2 dimensions.")
+        if inputs.shape != indexes.shape:
+            raise ValueError("`inputs` and `indexes` should have the same size.")
+        sym = self.quantize_symbols(inputs, means)
+        B = sym.shape[0]
+        idx = indexes.to(self.device, torch.int32).contiguous()
+        if int(idx.min()) < 0 or int(idx.max()) >= self._coder.ntables:
+            raise ValueError("index out of range")
+        enc = self._coder.encode(sym.view(B, -1), idx.view(B, -1))
+        return enc.to_bytes_list()
+
+    def decompress(self, strings, indexes, dtype=torch.float, means=None):
+        self._check_ready()
+        if not isinstance(strings, (tuple, list)):
+            raise ValueError("Invalid `strings` parameter type.")
+        if len(strings) != indexes.size(0):
+            raise ValueError("Invalid strings or indexes parameters")
+        if indexes.dim() < 2:
+            raise ValueError("Invalid `indexes` size. Expected a tensor with at least 2 dimensions.")
+        B = len(strings)
+        idx = indexes.to(self.device, torch.int32).contiguous()
+        enc = EncodedStreams.from_bytes_list([bytes(x) for x in strings], self.device)
+        sym = self._coder.decode(enc, idx.view(B, -1)).view(indexes.shape)
+        return self.dequantize(sym, means, dtype)
+
+
+class EntropyBottleneck(_CompressaiEntropyModel):
+    """compressai ``EntropyBottleneck`` surface over DVC's per-channel BitEstimator CDF
+    (bitEstimator.py:27-42): tables from ``FactorizedTables`` (medians 0), symbols = round(x),
+    table index = channel."""
+
+    def __init__(self, params, device=None):
+        super().__init__(device)
+        self.params = params  # [11, C] BitEstimator parameters (net.BitEstimator.params())
+        self.channels = int(params.shape[1])
+
+    def update(self, force=False):
+        if self._coder is not None and not force:
+            return False
+        t = FactorizedTables(torch.as_tensor(self.params).detach().cpu().numpy())
+        self._set_tables(t.cdf, t.cdf_length, t.offset)
+        return True
+
+    def _build_indexes(self, size):
+        return torch.arange(self.channels, dtype=torch.int32, device=self.device).view(1, -1, *([1] * (len(size) - 2))).expand(size).contiguous()
+
+    def compress(self, x):
+        return super().compress(x, self._build_indexes(x.size()))
+
+    def decompress(self, strings, size):
+        output_size = (len(strings), self.channels, *size)
+        return super().decompress(strings, self._build_indexes(output_size))
+
+
+class ConditionalEntropyModel(_CompressaiEntropyModel):
+    """compressai ``GaussianConditional`` surface: ``update_scale_table``, ``update``,
+    ``build_indexes(scales)``; ``dist`` = 'laplace' (DVC's feature likelihood, net.py:138-141;
+    LaplaceTables) or 'gaussian' (compressai's own, used by RLVC's RPM; GaussianTables)."""
+
+    def __init__(self, scale_table=None, dist="laplace", device=None):
+        super().__init__(device)
+        self.dist = dist
+        self.scale_table = None if scale_table is None else torch.as_tensor(scale_table, dtype=torch.float32)
+        self._table_dev = None
+
+    def update_scale_table(self, scale_table, force=False):
+        if self._coder is not None and not force:
+            return False
+        self.scale_table = torch.as_tensor(scale_table, dtype=torch.float32)
+        self.update()
+        return True
+
+    def update(self):
+        st = self.scale_table if self.scale_table is not None else get_scale_table()
+        t = LaplaceTables(st) if self.dist == "laplace" else GaussianTables(st)
+        self._set_tables(t.cdf, t.cdf_length, t.offset)
+        self._table_dev = torch.from_numpy(np.ascontiguousarray(t.scale_table, np.float32)).to(self.device)
+
+    def build_indexes(self, scales):
+        self._check_ready()
+        s = scales.float().contiguous()
+        K._chk(s, name="scales")
+        idx = torch.empty(s.shape, dtype=torch.int32, device=s.device)
+        _lib.call("fvc_build_indexes_flat", s.data_ptr(), self._table_dev.data_ptr(), self._table_dev.numel(),
+                  idx.data_ptr(), s.numel(), K.stream_handle())
+        return idx
+
+
+class GaussianTables:
+    """compressai ``GaussianConditional.update()`` (entropy_models.py:18-23 scale table): float32
+    torch arithmetic on the host as compressai computes it (multiplier = -Phi^-1(tail_mass/2),
+    pmf = Phi((.5-|k|)/s) - Phi((-.5-|k|)/s), Phi(x) = .5 erfc(-x/sqrt 2))."""
+
+    def __init__(self, scale_table=None, tail_mass: float = TAIL_MASS):
+        import scipy.stats
+        st = torch.as_tensor(scale_table if scale_table is not None else get_scale_table(), dtype=torch.float32).cpu()
+        self.scale_table = st.numpy().astype(np.float32)
+        multiplier = -float(scipy.stats.norm.ppf(tail_mass / 2))
+        pmf_center = torch.ceil(st * multiplier).int()
+        pmf_length = 2 * pmf_center + 1
+        max_length = int(pmf_length.max())
+        samples = torch.abs(torch.arange(max_length).int() - pmf_center[:, None]).float()
+        s = st.unsqueeze(1).float()
+        cum = lambda v: 0.5 * torch.erfc(-(2 ** -0.5) * v)
+        upper = cum((0.5 - samples) / s)
+        lower = cum((-0.5 - samples) / s)
+        pmf = (upper - lower).numpy()
+        tails = (2 * lower[:, 0]).numpy()
+        lengths = pmf_length.numpy().astype(np.int64)
+        self.cdf = _pack_tables(pmf, tails, lengths)
+        self.cdf_length = (lengths + 2).astype(np.int32)
+        self.offset = (-pmf_center.numpy()).astype(np.int32)
+
+
+class RecProbModel:
+    """``entropy_models.py:26-94`` RecProbModel surface (the coder API the reference's RLVC path
+    calls): ``update(scale_table=None, force=False)``, ``compress(x) -> list[bytes]`` (one string
+    per batch item over (C,H,W)), ``decompress(strings, shape)``, ``get_actual_bits(strings)``,
+    ``get_estimate_bits(likelihoods)``. ``RPM_flag`` False: factorized entropy bottleneck;
+    True: conditional model on ``self.sigma`` / ``self.mu`` set by the caller (RPM or, for DVC,
+    the hyperprior's sigma with mu = None)."""
+
+    def __init__(self, channels, bit_estimator_params=None, dist="gaussian", device=None):
+        self.channels = int(channels)
+        self.sigma = self.mu = self.prior_latent = None
+        self.RPM_flag = False
+        self.entropy_bottleneck = (EntropyBottleneck(bit_estimator_params, device)
+                                   if bit_estimator_params is not None else None)
+        self.gaussian_conditional = ConditionalEntropyModel(None, dist, device)
+
+    def set_RPM(self, RPM_flag):
+        self.RPM_flag = RPM_flag
+
+    def update(self, scale_table=None, force=False):
+        if scale_table is None:
+            scale_table = get_scale_table()
+        updated = self.gaussian_conditional.update_scale_table(scale_table, force=force)
+        if self.entropy_bottleneck is not None:
+            updated |= self.entropy_bottleneck.update(force=force)
+        return updated
+
+    def get_actual_bits(self, string):
+        return torch.tensor(float(len(b"".join(string)) * 8))
+
+    def get_estimate_bits(self, likelihoods):
+        return torch.sum(torch.clamp(-1.0 * torch.log(likelihoods + 1e-5) / math.log(2.0), 0, 50))
+
+    def compress(self, x):
+        if self.RPM_flag:
+            indexes = self.gaussian_conditional.build_indexes(self.sigma)
+            return self.gaussian_conditional.compress(x, indexes, means=self.mu)
+        return self.entropy_bottleneck.compress(x)
+
+    def decompress(self, string, shape):
+        if self.RPM_flag:
+            indexes = self.gaussian_conditional.build_indexes(self.sigma)
+            return self.gaussian_conditional.decompress(string, indexes, means=self.mu)
+        return self.entropy_bottleneck.decompress(string, shape)

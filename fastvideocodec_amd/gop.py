@@ -72,23 +72,70 @@ def encode_decode_gop(model, frames: torch.Tensor, check=False, overlap=True, jo
     wait for this GOP's coder/decoder tail, so the next GOP's encoder starts while the last
     frames are still being range-decoded and reconstructed; every tensor that crosses streams is
     record_stream'ed, and the caller synchronises the device (or waits on the side streams via
-    join_side_streams) before reading the returned bitstreams / recons."""
+    join_side_streams) before reading the returned bitstreams / recons.
+
+    Split-precision overflow: after each frame's encoder pass a non-blocking probe copies the
+    encoder stream's overflow flag to pinned memory. join=True resolves the probes at the end:
+    on a hit the GOP is re-coded on the fp32 kernels (model.on_overflow == "recompute"; its
+    bitstreams then carry precision 'f32') or FvcError is raised. join=False leaves the probes
+    on the model; the caller resolves them with check_overflow(model) after synchronising."""
+    if join:
+        pending = getattr(model, "_overflow_probes", [])
+        model._overflow_probes = []
+        err = None
+        try:
+            out = _encode_decode_gop(model, frames, check, overlap, join)
+        except _lib.FvcError as e:  # e.g. a corrupt-stream check tripped by an overflowed frame
+            err = e
+        hit = any(p.result() for p in model._overflow_probes)
+        model._overflow_probes = pending
+        if err is not None and not hit:
+            raise err
+        if hit and K.conv_precision() != "f32":
+            model.overflow_events = getattr(model, "overflow_events", 0) + 1
+            if model.on_overflow == "raise":
+                raise _lib.FvcError("split-precision conv operand overflow in a GOP")
+            with K.precision("f32"):
+                return encode_decode_gop(model, frames, check, overlap, join)
+        return out
+    return _encode_decode_gop(model, frames, check, overlap, join)
+
+
+def check_overflow(model) -> bool:
+    """Resolve the overflow probes of join=False GOPs (waits for their copies). Raises FvcError
+    on a hit: streamed bitstreams cannot be re-coded after the fact."""
+    probes = getattr(model, "_overflow_probes", [])
+    model._overflow_probes = []
+    if any(p.result() for p in probes):
+        model.overflow_events = getattr(model, "overflow_events", 0) + 1
+        raise _lib.FvcError("split-precision conv operand overflow in a streamed GOP; re-code it "
+                            "with kernels.precision('f32')")
+    return False
+
+
+def _encode_decode_gop(model, frames, check, overlap, join):
     G, T = frames.shape[:2]
     main = torch.cuda.current_stream(frames.device)
     if overlap:
         s_cd0, s_cd1, s_rec = _side_streams(frames.device)
     else:
         s_cd0 = s_cd1 = s_rec = main
-    _lib.call("fvc_x3_set_cu_reserve", PIPELINE_CU_RESERVE if overlap else 0)
+    if not hasattr(model, "_overflow_probes"):
+        model._overflow_probes = []
+    if K.conv_precision() != "f32":
+        K.overflow_flag(frames.device).zero_()
     x_enc = frames[:, 0].contiguous()
     x_dec = x_enc
     bitstreams, decoded, sses, enc_recons, keep = [], [], [], [], [x_enc]
     model.update()
-    with torch.no_grad():
+    # launches outside the pipeline get the whole GPU: the reserve applies inside this block only
+    with torch.no_grad(), K.cu_reserve(PIPELINE_CU_RESERVE if overlap else 0):
         for t in range(1, T):
             cur = frames[:, t].contiguous()
             tens = model._encode_graph(cur, x_enc)
             clipped, sse = K.recon_finalize(tens["recon"], tens["cur4"], tens["warpframe"], tens["prediction"])
+            if K.conv_precision() != "f32":
+                model._overflow_probes.append(K.OverflowProbe(frames.device))
             lat = {k: tens[k] for k in ("mvfeature", "z", "feature", "sigma")}
             del tens
             s_cd = s_cd0 if t % 2 else s_cd1
@@ -110,7 +157,6 @@ def encode_decode_gop(model, frames: torch.Tensor, check=False, overlap=True, jo
             enc_recons.append(clipped)
             sses.append(sse)
             x_enc, x_dec = clipped, rec_dec
-    _lib.call("fvc_x3_set_cu_reserve", 0)  # launches outside the pipeline get the whole GPU
     if join:
         join_side_streams(frames.device)
     return bitstreams, decoded, sses, enc_recons

@@ -6,6 +6,7 @@ kernels trust their arguments (an out-of-bounds launch can fault the whole GPU).
 """
 from __future__ import annotations
 
+import contextlib
 import os
 
 import torch
@@ -143,14 +144,78 @@ def gdn(x, beta, gamma, inverse):
 
 
 # ------------------------------------------------------------------ conv
+PRECISIONS = ("x3", "f32")
+_STATE = {"precision": None, "cu_reserve": 0}
+
+
 def conv_precision() -> str:
     """'x3' (default): split-precision fp16 matrix-core kernel (fvc_conv_x3.hip) wherever the
-    layer supports it; 'f32': the fp32-MFMA kernel everywhere (FVC_CONV_PRECISION=f32)."""
-    import os
-    p = os.environ.get("FVC_CONV_PRECISION", "x3")
-    if p not in ("x3", "f32"):
+    layer supports it; 'f32': the fp32-MFMA kernel everywhere (FVC_CONV_PRECISION=f32, or inside
+    ``with precision('f32')``, which the codec uses to recompute a frame whose activations left
+    the split-precision range)."""
+    p = _STATE["precision"] or os.environ.get("FVC_CONV_PRECISION", "x3")
+    if p not in PRECISIONS:
         raise ValueError(f"FVC_CONV_PRECISION must be x3 or f32, got {p!r}")
     return p
+
+
+@contextlib.contextmanager
+def precision(p: str | None):
+    """Override the conv precision for convs packed / run inside the block (None: no override)."""
+    if p is not None and p not in PRECISIONS:
+        raise ValueError(p)
+    old = _STATE["precision"]
+    _STATE["precision"] = p if p is not None else old
+    try:
+        yield
+    finally:
+        _STATE["precision"] = old
+
+
+@contextlib.contextmanager
+def cu_reserve(n: int):
+    """CUs the split-precision conv's persistent grid leaves to other streams' kernels, for the
+    convs launched inside the block (gop.py's pipeline)."""
+    old = _STATE["cu_reserve"]
+    _STATE["cu_reserve"] = int(n)
+    try:
+        yield
+    finally:
+        _STATE["cu_reserve"] = old
+
+
+_OVF = {}
+
+
+def overflow_flag(device=None) -> torch.Tensor:
+    """The split-precision overflow flag (device int32[1]) of the current stream of device: every
+    x3 conv launched on that stream ORs 1 into it if it staged |v| >= 65000 (or a non-finite v)."""
+    st = torch.cuda.current_stream(device)
+    key = (str(st.device), st.cuda_stream)
+    if key not in _OVF:
+        _OVF[key] = torch.zeros(1, dtype=torch.int32, device=st.device)
+    return _OVF[key]
+
+
+class OverflowProbe:
+    """Non-blocking read of a stream's overflow flag: copies it to pinned host memory behind the
+    work already queued; ``result()`` waits for that copy only (not the device)."""
+
+    def __init__(self, device=None, reset=True):
+        flag = overflow_flag(device)
+        self.host = torch.empty(1, dtype=torch.int32, pin_memory=True)
+        self.host.copy_(flag, non_blocking=True)
+        self.event = torch.cuda.Event()
+        self.event.record()
+        if reset:
+            flag.zero_()
+
+    def ready(self) -> bool:
+        return self.event.query()
+
+    def result(self) -> bool:
+        self.event.synchronize()
+        return bool(self.host.item())
 
 
 class PackedConv:
@@ -236,7 +301,7 @@ class PackedConv:
             fn = "fvc_deconv2d_nhwc_x3" if self.transposed else "fvc_conv2d_nhwc_x3"
             _lib.call(fn, x.data_ptr(), self.wpack.data_ptr(), self.osc, self.bias.data_ptr(), _ptr(res),
                       y.data_ptr(), B, H, W, self.cin, self.cout, self.ksize, self.stride, in_op, act, post,
-                      stream_handle())
+                      _STATE["cu_reserve"], overflow_flag(x.device).data_ptr(), stream_handle())
         else:
             fn = "fvc_deconv2d_nhwc_f32" if self.transposed else "fvc_conv2d_nhwc_f32"
             _lib.call(fn, x.data_ptr(), self.wpack.data_ptr(), self.bias.data_ptr(), _ptr(res), y.data_ptr(), B, H,
@@ -254,13 +319,10 @@ class PackedConv:
         return y
 
 
-def x3_overflow(reset: bool = True) -> bool:
-    """True if any split-precision conv staged an activation with |v| >= 65000 since the last
-    reset (synchronises the device)."""
-    import ctypes
-    flag = ctypes.c_int(0)
-    _lib.call("fvc_x3_overflow_flag", ctypes.addressof(flag), int(reset))
-    return bool(flag.value)
+def x3_overflow(reset: bool = True, device=None) -> bool:
+    """True if any split-precision conv on the current stream staged an activation with
+    |v| >= 65000 since the last reset (waits for the stream's queued work)."""
+    return OverflowProbe(device, reset).result()
 
 
 # ------------------------------------------------------------------ reductions

@@ -7,13 +7,17 @@ returns a ``VideoCompressor`` carrying the attributes the reference GOP driver r
 signatures and return values, so ``eval.py``'s ``static_simulation_model`` can call them
 unchanged.
 
-The I-frame codec (BPG via ``os.system``, models.py:412-429) is out of scope: ``I_compression``
-passes the I-frame through losslessly and reports bpp 0 / PSNR inf (documented in DESIGN.md).
+The I-frame codec (BPG via ``os.system``, models.py:412-429) is replaced by a pass-through:
+``I_compression`` returns the I-frame losslessly with bpp 0 / PSNR inf, and
+``parallel_compression`` leaves a pass-through I-frame out of its aggregates even when
+``compressI`` is set (an infinite PSNR would otherwise swamp ``psnr``), so eval.py's averages
+stay finite (documented in DESIGN.md).
 """
 from __future__ import annotations
 
 import math
 import os
+import warnings
 
 import torch
 
@@ -24,22 +28,42 @@ _RATIO_LIST = [256, 512, 1024, 2048, 2048 * 2, 2048 * 4, 2048 * 8]
 _I_LVL_LIST = [37, 32, 27, 22, 17, 12, 7]
 
 
+class SeededWeightsWarning(UserWarning):
+    """The codec runs on the build's seeded (untrained) weights, not a DVC snapshot."""
+
+
 def get_DVC_pretrained(level, checkpoint=None, seed=20261015, device=None):
-    """models.py:1432-1445. The reference loads DVC/snapshot/{r}.model (absent offline); here a
-    checkpoint path may be given, otherwise the build's seeded weights are used."""
+    """models.py:1432-1445. The reference loads DVC/snapshot/{r}.model through
+    DVC/net.py:21-34 load_model (the snapshots are absent from the reference tree). Here:
+    checkpoint=path loads a state_dict the same way (keys the model does not have are dropped,
+    as load_model does; they are listed in ``model.dropped_checkpoint_keys``) and a missing file
+    raises FileNotFoundError like load_model's open(); checkpoint=None uses the build's seeded
+    weights, flagged by ``model.weights_source == 'seeded'`` and a SeededWeightsWarning."""
     model = VideoCompressor()
     model.name = "DVC-pretrained"
     model.compression_level = level
     model.loss_type = "P"
     model.I_level = _I_LVL_LIST[level]
     model.r = _RATIO_LIST[level]
-    if checkpoint is not None and os.path.isfile(checkpoint):
+    if checkpoint is not None:
+        if not os.path.isfile(checkpoint):
+            raise FileNotFoundError(f"DVC checkpoint not found: {checkpoint}")
         sd = torch.load(checkpoint, map_location="cpu", weights_only=True)
         own = model.state_dict()
+        model.dropped_checkpoint_keys = sorted(k for k in sd if k not in own)
+        missing = sorted(k for k in own if k not in sd)
         own.update({k: v for k, v in sd.items() if k in own})  # net.py:21-34 load_model semantics
         model.load_state_dict(own)
+        if model.dropped_checkpoint_keys or missing:
+            warnings.warn(f"checkpoint {checkpoint}: {len(model.dropped_checkpoint_keys)} unknown keys dropped, "
+                          f"{len(missing)} model keys kept at their initial values", stacklevel=2)
+        model.weights_source = checkpoint
     else:
         model.load_state_dict(seeded_torch_state_dict(seed))
+        model.dropped_checkpoint_keys = []
+        model.weights_source = "seeded"
+        warnings.warn(f"DVC-pretrained level {level}: no checkpoint given, using seeded weights (seed {seed}); "
+                      "rate-distortion figures are not those of a trained DVC", SeededWeightsWarning, stacklevel=2)
     dev = device if device is not None else (torch.device("cuda") if torch.cuda.is_available() else None)
     if dev is not None:
         model = model.to(dev)
@@ -88,7 +112,8 @@ def PSNR(Y1_raw, Y1_com, use_list=False):
 
 
 def I_compression(Y1_raw, I_level, model_name=""):
-    """models.py:412-429 calls bpgenc/bpgdec; BPG is out of scope: lossless pass-through."""
+    """models.py:412-429 calls bpgenc/bpgdec; BPG is out of scope: lossless pass-through
+    (bpp 0, PSNR inf)."""
     return Y1_raw, torch.zeros((), device=Y1_raw.device), torch.full((), float("inf"), device=Y1_raw.device)
 
 
@@ -107,7 +132,9 @@ def parallel_compression(args, model, data, compressI=False, level=0, batch_idx=
     aux_loss_list, aux2_loss_list = [], []
     x_hat, bpp_i, psnr_i = I_compression(data[0:1], model.I_level)
     data[0:1] = x_hat
-    if compressI:
+    if compressI and bool(torch.isfinite(psnr_i)):
+        # models.py:251-253; a lossless pass-through I-frame (PSNR inf, bpp 0) is left out of
+        # the aggregates instead: it would make psnr infinite and bias be_loss towards 0
         bpp_list += [bpp_i]
         psnr_list += [psnr_i]
     B = data.size(0)

@@ -24,6 +24,7 @@ import torch.nn as nn
 from torch.nn import Parameter
 
 from . import kernels as K
+from ._lib import FvcError
 from .entropy_models import FactorizedTables, LaplaceTables, RangeCoder, get_scale_table
 from .weights import OUT_CHANNEL_M, OUT_CHANNEL_MV, OUT_CHANNEL_N
 
@@ -38,16 +39,19 @@ class _ConvP(nn.Module):
         self.weight = Parameter(torch.zeros(shape), requires_grad=False)
         self.bias = Parameter(torch.zeros(cout), requires_grad=False)
         self.k, self.stride, self.transposed = k, stride, transposed
-        self._packed = None
+        self._packed = {}
 
     def packed(self) -> K.PackedConv:
-        if self._packed is None:
-            self._packed = K.PackedConv(self.weight, self.bias, self.k, self.stride, self.transposed,
-                                        self.weight.device)
-        return self._packed
+        """The weight pack for the active conv precision (x3 by default; f32 when a frame is
+        recomputed after a split-precision overflow), built once per precision."""
+        p = K.conv_precision()
+        if p not in self._packed:
+            self._packed[p] = K.PackedConv(self.weight, self.bias, self.k, self.stride, self.transposed,
+                                           self.weight.device, precision=p)
+        return self._packed[p]
 
     def invalidate(self):
-        self._packed = None
+        self._packed = {}
 
 
 class _GDNP(nn.Module):
@@ -289,15 +293,30 @@ class Synthesis_prior_net(nn.Module):
 
 
 # ------------------------------------------------------------------ the codec
-class PFrameBitstream:
-    """In-memory P-frame bitstream: three latents, one rANS stream per (frame, channel)."""
+FRAMINGS = ("channel", "item")
 
-    def __init__(self, mv, z, feature, batch, hw16, hw64):
+
+class PFrameBitstream:
+    """In-memory P-frame bitstream: three latents (mv, z, feature) of ``batch`` frames.
+
+    framing 'channel' (the codec's default): one rANS stream per (frame, latent, channel), so the
+    decoder runs C-way parallel per frame; 'item': compressai's framing (EntropyModel.compress,
+    entropy_models.py:80-86), one stream per (frame, latent) over the whole (C,H,W) latent in C
+    order. Either way each stream equals compressai's encode_with_indexes on its symbols.
+    precision: the conv precision the encoder's reconstruction used ('x3', or 'f32' when the
+    frame was recomputed after a split-precision overflow); the decoder must use the same."""
+
+    def __init__(self, mv, z, feature, batch, hw16, hw64, framing="channel", precision="x3"):
         self.mv, self.z, self.feature = mv, z, feature
         self.batch, self.hw16, self.hw64 = batch, hw16, hw64
+        self.framing, self.precision = framing, precision
 
     def nbytes(self) -> int:
         return int((self.mv.pack_off[-1] + self.z.pack_off[-1] + self.feature.pack_off[-1]).item()) * 4
+
+    def check(self):
+        for part in (self.mv, self.z, self.feature):
+            part.check()
 
 
 class VideoCompressor(nn.Module):
@@ -394,40 +413,71 @@ class VideoCompressor(nn.Module):
                     prediction=prediction, warpframe=warpframe, feature=feature, z=z, sigma=sigma,
                     recon=recon)
 
+    # -- split-precision overflow: every x3 conv ORs into its stream's flag;
+    # a frame that set it is recomputed on the fp32 kernels (on_overflow="recompute", default)
+    # or rejected (on_overflow="raise")
+    on_overflow = "recompute"
+
+    def _run_checked(self, fn):
+        """Run fn() (a frame's encoder-side work on the current stream) and check the stream's
+        overflow flag once its work is done: a copy to pinned memory behind the queued kernels,
+        then a wait for that copy only. Returns (result, precision used)."""
+        if K.conv_precision() == "f32":
+            return fn(), "f32"
+        K.overflow_flag().zero_()
+        out = fn()
+        if not K.OverflowProbe().result():
+            return out, "x3"
+        self.overflow_events = getattr(self, "overflow_events", 0) + 1
+        if self.on_overflow == "raise":
+            raise FvcError("split-precision conv operand overflow (|activation| >= 65000); "
+                           "set on_overflow='recompute' or FVC_CONV_PRECISION=f32")
+        with K.precision("f32"):
+            return fn(), "f32"
+
     def forward(self, input_image, referframe, quant_noise_feature=None, quant_noise_z=None,
                 quant_noise_mv=None, return_intermediates=False):
         if self.training:
             raise NotImplementedError("training-mode forward (additive quantisation noise) is out of scope")
         self._check_frames(input_image, referframe)
         with torch.no_grad():
-            t = self._encode_graph(input_image, referframe)
-            B, _, H, W = input_image.shape
-            clipped, sse = K.recon_finalize(t["recon"], t["cur4"], t["warpframe"], t["prediction"])
-            npx = B * H * W
-            if self.calrealbits:
-                bs = self.compress_tensors(t)
-                bits_f = bs.feature.pack_off[-1:].double() * 32
-                bits_z = bs.z.pack_off[-1:].double() * 32
-                bits_mv = bs.mv.pack_off[-1:].double() * 32
-            else:
-                bz, bmv = self._be_params()
-                bits_f = K.bits_laplace(t["feature"], t["sigma"], OUT_CHANNEL_M)
-                bits_z = K.bits_factorized(t["z"], bz, OUT_CHANNEL_N)
-                bits_mv = K.bits_factorized(t["mvfeature"], bmv, OUT_CHANNEL_MV)
-            mse_loss = (sse[0] / (3 * npx)).float()
-            warploss = (sse[1] / (3 * npx)).float()
-            interloss = (sse[2] / (3 * npx)).float()
-            bpp_feature = (bits_f[0] / npx).float()
-            bpp_z = (bits_z[0] / npx).float()
-            bpp_mv = (bits_mv[0] / npx).float()
-            bpp = bpp_feature + bpp_z + bpp_mv
-        out = (clipped, mse_loss, warploss, interloss, bpp_feature, bpp_z, bpp_mv, bpp)
+            (out, t), self.last_precision = self._run_checked(
+                lambda: self._forward_impl(input_image, referframe))
         if return_intermediates:
             return out, t
         return out
 
+    def _forward_impl(self, input_image, referframe):
+        t = self._encode_graph(input_image, referframe)
+        B, _, H, W = input_image.shape
+        clipped, sse = K.recon_finalize(t["recon"], t["cur4"], t["warpframe"], t["prediction"])
+        npx = B * H * W
+        if self.calrealbits:
+            bs = self.compress_tensors(t)
+            bits_f = bs.feature.pack_off[-1:].double() * 32
+            bits_z = bs.z.pack_off[-1:].double() * 32
+            bits_mv = bs.mv.pack_off[-1:].double() * 32
+        else:
+            bz, bmv = self._be_params()
+            bits_f = K.bits_laplace(t["feature"], t["sigma"], OUT_CHANNEL_M)
+            bits_z = K.bits_factorized(t["z"], bz, OUT_CHANNEL_N)
+            bits_mv = K.bits_factorized(t["mvfeature"], bmv, OUT_CHANNEL_MV)
+        mse_loss = (sse[0] / (3 * npx)).float()
+        warploss = (sse[1] / (3 * npx)).float()
+        interloss = (sse[2] / (3 * npx)).float()
+        bpp_feature = (bits_f[0] / npx).float()
+        bpp_z = (bits_z[0] / npx).float()
+        bpp_mv = (bits_mv[0] / npx).float()
+        bpp = bpp_feature + bpp_z + bpp_mv
+        return (clipped, mse_loss, warploss, interloss, bpp_feature, bpp_z, bpp_mv, bpp), t
+
     # ---------------------------------------------------------------- real bitstream
-    def compress_tensors(self, t) -> PFrameBitstream:
+    def compress_tensors(self, t, framing="channel") -> PFrameBitstream:
+        """Range-code the latents of an encoder pass (NHWC device tensors mvfeature, z, feature,
+        sigma). framing: 'channel' (one stream per frame x channel, the codec's default) or 'item'
+        (compressai's one string per frame per latent)."""
+        if framing not in FRAMINGS:
+            raise ValueError(f"framing must be one of {FRAMINGS}")
         self.update()
         c = self._coders
         B, H16, W16, _ = t["mvfeature"].shape
@@ -438,19 +488,26 @@ class VideoCompressor(nn.Module):
         idx_mv = K.channel_indexes(B, H16 * W16, OUT_CHANNEL_MV, sym_mv.device)
         idx_z = K.channel_indexes(B, H64 * W64, OUT_CHANNEL_N, sym_z.device)
         idx_f = K.build_indexes(t["sigma"], c["scale_table"], OUT_CHANNEL_M)
-        enc_mv = c["mv"].encode(sym_mv.view(-1, H16 * W16), idx_mv.view(-1, H16 * W16))
-        enc_z = c["z"].encode(sym_z.view(-1, H64 * W64), idx_z.view(-1, H64 * W64))
-        enc_f = c["feature"].encode(sym_f.view(-1, H16 * W16), idx_f.view(-1, H16 * W16))
-        return PFrameBitstream(enc_mv, enc_z, enc_f, B, (H16, W16), (H64, W64))
+        # symbols are [B, C, HW] in memory either way: the framing only chooses the stream cut
+        rows = (lambda C, hw: (B * C, hw)) if framing == "channel" else (lambda C, hw: (B, C * hw))
+        enc_mv = c["mv"].encode(sym_mv.view(rows(OUT_CHANNEL_MV, H16 * W16)), idx_mv.view(rows(OUT_CHANNEL_MV, H16 * W16)))
+        enc_z = c["z"].encode(sym_z.view(rows(OUT_CHANNEL_N, H64 * W64)), idx_z.view(rows(OUT_CHANNEL_N, H64 * W64)))
+        enc_f = c["feature"].encode(sym_f.view(rows(OUT_CHANNEL_M, H16 * W16)), idx_f.view(rows(OUT_CHANNEL_M, H16 * W16)))
+        return PFrameBitstream(enc_mv, enc_z, enc_f, B, (H16, W16), (H64, W64), framing, K.conv_precision())
 
-    def compress(self, input_image, referframe, return_sse=False):
+    def compress(self, input_image, referframe, return_sse=False, framing="channel"):
         """Encode one P-frame: returns (bitstream, clipped_recon[, sse]). The recon is what
         ``decompress`` reproduces bit-for-bit; sse = device doubles {recon, warp, pred} SSE."""
         self._check_frames(input_image, referframe)
-        with torch.no_grad():
+
+        def run():
             t = self._encode_graph(input_image, referframe)
-            bs = self.compress_tensors(t)
+            bs = self.compress_tensors(t, framing)
             clipped, sse = K.recon_finalize(t["recon"], t["cur4"], t["warpframe"], t["prediction"])
+            return bs, clipped, sse
+
+        with torch.no_grad():
+            (bs, clipped, sse), self.last_precision = self._run_checked(run)
         if return_sse:
             return bs, clipped, sse
         return bs, clipped
@@ -464,23 +521,24 @@ class VideoCompressor(nn.Module):
         B = bs.batch
         (H16, W16), (H64, W64) = bs.hw16, bs.hw64
         dev = bs.mv.packed.device
-        with torch.no_grad():
+        rows = (lambda C, hw: (B * C, hw)) if bs.framing == "channel" else (lambda C, hw: (B, C * hw))
+        with torch.no_grad(), K.precision(bs.precision):
             idx_z = K.channel_indexes(B, H64 * W64, OUT_CHANNEL_N, dev)
-            sym_z = c["z"].decode(bs.z, idx_z.view(-1, H64 * W64), check).view(B, OUT_CHANNEL_N, H64 * W64)
+            sym_z = c["z"].decode(bs.z, idx_z.view(rows(OUT_CHANNEL_N, H64 * W64)), check).view(B, OUT_CHANNEL_N, H64 * W64)
             z = K.symbols_to_latent(sym_z, H64, W64, OUT_CHANNEL_N)
             sigma = self.respriorDecoder.run(z)
             idx_f = K.build_indexes(sigma, c["scale_table"], OUT_CHANNEL_M)
-            sym_f = c["feature"].decode(bs.feature, idx_f.view(-1, H16 * W16), check).view(B, OUT_CHANNEL_M, H16 * W16)
+            sym_f = c["feature"].decode(bs.feature, idx_f.view(rows(OUT_CHANNEL_M, H16 * W16)), check).view(B, OUT_CHANNEL_M, H16 * W16)
             feature = K.symbols_to_latent(sym_f, H16, W16, OUT_CHANNEL_M)
             idx_mv = K.channel_indexes(B, H16 * W16, OUT_CHANNEL_MV, dev)
-            sym_mv = c["mv"].decode(bs.mv, idx_mv.view(-1, H16 * W16), check).view(B, OUT_CHANNEL_MV, H16 * W16)
+            sym_mv = c["mv"].decode(bs.mv, idx_mv.view(rows(OUT_CHANNEL_MV, H16 * W16)), check).view(B, OUT_CHANNEL_MV, H16 * W16)
             mvq = K.symbols_to_latent(sym_mv, H16, W16, OUT_CHANNEL_MV)
-        return {"mv": mvq, "feature": feature, "z": z}
+        return {"mv": mvq, "feature": feature, "z": z, "precision": bs.precision}
 
     def reconstruct(self, lat, referframe):
         """Decoder synthesis from decoded latents: mvDecoder -> motion compensation ->
         resDecoder (+ prediction) -> clamp. Returns the NCHW reconstruction."""
-        with torch.no_grad():
+        with torch.no_grad(), K.precision(lat.get("precision")):
             ref4 = K.nchw_to_nhwc(referframe.float().contiguous(), 4)
             mv_up = self.mvDecoder.run(lat["mv"])
             prediction, _ = self.motioncompensation(ref4, mv_up)

@@ -4,7 +4,10 @@
  * Every entry point is `extern "C"`, takes plain pointers + sizes + a hipStream_t, never
  * allocates, never throws, and returns 0 on success or a negative code
  * (-hipError_t, or FVC_E*). Device pointers are caller-owned (torch tensors in the Python
- * host layer); calls are stream-ordered and reentrant per stream.
+ * host layer); calls are stream-ordered and reentrant: the library keeps no mutable state
+ * between calls (launch policy such as the CU reserve and status flags such as the
+ * split-precision overflow flag are arguments), so concurrent calls on different streams or
+ * host threads do not interact.
  *
  * Activation layout inside the codec is NHWC fp32 with the channel count padded to a
  * multiple of 4 ("cp"; pad channels are written as zeros). Frames at the module boundary
@@ -77,27 +80,25 @@ int fvc_deconv2d_nhwc_f32(const float* x, const float* wpack, const float* bias,
  * product (fp32-level accuracy, ~1e-6 relative). Taken for layers with cin padded to a multiple
  * of 8 and cout > 4 (fvc_conv_x3_supported). The pack is fp16 pairs plus a per-layer output
  * scale osc = 2^-kw (weights are pre-scaled by 2^kw). Activations must stay below 65000 in
- * magnitude: staging raises a device flag otherwise, read (and optionally reset) with
- * fvc_x3_overflow_flag (synchronous). */
+ * magnitude: a launch that stages a larger (or non-finite) value ORs 1 into *overflow_flag
+ * (a caller-owned device int; NULL = unchecked) and its output must be recomputed on the fp32
+ * kernels (the Python layer does this, net.py). cu_reserve (>= 0): CUs the persistent grid
+ * leaves to kernels of other streams (capped at half the CUs). A pipelined caller (encoder +
+ * coder + decoder streams in flight, fastvideocodec_amd/gop.py) passes it so that a conv block
+ * never waits for a CU held by a long-running rANS chain, which would double that launch's
+ * time; 0 = the whole GPU. */
 int fvc_conv_x3_supported(int cin, int cout, int ksize, int stride, int transposed);
 size_t fvc_conv_x3_wpack_bytes(int cin, int cout, int ksize, int stride, int transposed);
 int fvc_conv_x3_pack_weight(const float* w_host, void* wpack_host, float* osc_out, int cin,
                             int cout, int ksize, int stride, int transposed);
 int fvc_conv2d_nhwc_x3(const float* x, const void* wpack, float osc, const float* bias,
                        const float* res, float* y, int batch, int h, int w, int cin, int cout,
-                       int ksize, int stride, int in_op, int act, int post_op,
-                       fvc_stream_t stream);
+                       int ksize, int stride, int in_op, int act, int post_op, int cu_reserve,
+                       int* overflow_flag, fvc_stream_t stream);
 int fvc_deconv2d_nhwc_x3(const float* x, const void* wpack, float osc, const float* bias,
                          const float* res, float* y, int batch, int h, int w, int cin, int cout,
-                         int ksize, int stride, int in_op, int act, int post_op,
-                         fvc_stream_t stream);
-int fvc_x3_overflow_flag(int* host_flag, int reset);
-/* CUs the split-precision conv's persistent grid leaves to kernels of other streams (default 0;
- * capped at half the CUs). A pipelined caller (encoder + coder + decoder streams in flight, see
- * fastvideocodec_amd/gop.py) sets it so that a conv block never waits for a CU held by a
- * long-running rANS chain, which would double that launch's time. Host-side setting, applies to
- * subsequent launches. */
-int fvc_x3_set_cu_reserve(int ncu);
+                         int ksize, int stride, int in_op, int act, int post_op, int cu_reserve,
+                         int* overflow_flag, fvc_stream_t stream);
 
 /* ------------------------------------------------------------------ layout / resampling */
 int fvc_nchw_to_nhwc(const float* src, float* dst, int batch, int c, int h, int w, int cp,
@@ -172,6 +173,14 @@ int fvc_build_indexes(const float* sigma, const float* scale_table, int n_scales
                       int batch, int h, int w, int c, int cp, fvc_stream_t stream);
 /* per-channel table index for factorized latents: idx[b][ch][i] = ch */
 int fvc_channel_indexes(int32_t* idx, int batch, int hw, int c, fvc_stream_t stream);
+/* Elementwise over n values of any contiguous layout (the compressai-framed API, NCHW):
+ * EntropyModel.quantize(x, "symbols", means): sym = round_half_even(x - means) (means may be NULL);
+ * EntropyModel.dequantize: out = sym + means; GaussianConditional.build_indexes on a flat array. */
+int fvc_quantize_symbols(const float* x, const float* means, int32_t* sym, size_t n, fvc_stream_t stream);
+int fvc_dequantize_symbols(const int32_t* sym, const float* means, float* out, size_t n,
+                           fvc_stream_t stream);
+int fvc_build_indexes_flat(const float* scales, const float* scale_table, int n_scales, int32_t* idx,
+                           size_t n, fvc_stream_t stream);
 
 /* host: compressai pmf_to_quantized_cdf; cdf_out has n+1 entries. */
 int fvc_pmf_to_quantized_cdf(const float* pmf, int n, int precision, uint32_t* cdf_out);
@@ -189,9 +198,12 @@ int fvc_rans_encode(const int32_t* symbols, const int32_t* indexes, const int64_
                     const int32_t* cdf_sizes, const int32_t* offsets, void* ws, uint32_t* words,
                     const int64_t* word_off, int32_t* nwords, fvc_stream_t stream);
 /* Pack encoded regions into one contiguous buffer: out[pack_off[s] ..] = last nwords[s] words
- * of region s; pack_off is [nstreams+1] (exclusive scan of nwords, computed on device). */
+ * of region s; pack_off is [nstreams+1] (exclusive scan of nwords, computed on device).
+ * status (device int, may be NULL) = 0, or FVC_ENOSPC if any stream ran out of space (such a
+ * stream packs as empty; the caller must not ship the result). */
 int fvc_rans_pack(const uint32_t* words, const int64_t* word_off, const int32_t* nwords,
-                  int nstreams, int64_t* pack_off, uint32_t* out, fvc_stream_t stream);
+                  int nstreams, int64_t* pack_off, uint32_t* out, int32_t* status,
+                  fvc_stream_t stream);
 /* Decode tables, built once per table set (fvc_rans_lut_bytes(ntables, cdf_stride) bytes): per
  * table a 4096-bucket cum -> first-candidate-symbol map and a start|freq<<16 word per symbol
  * (L2-resident; a decoded symbol costs two dependent cache hits). */

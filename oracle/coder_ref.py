@@ -3,6 +3,9 @@
 * ``pmf_to_quantized_cdf_py`` / ``rans_encode_py`` / ``rans_decode_py``: pure-Python
   restatements of compressai 1.2's C++ coder (cpp_exts/ops/ops.cpp, rans_interface.cpp,
   ryg_rans rans64.h) for small known-answer cases;
+* ``pmf_to_quantized_cdf_np``: the quantiser restated on the frequency array (numpy), fast
+  enough for every real table; the product's host quantiser edits the cumulative table in place
+  instead, so the two are independent programs for one spec;
 * ``CRef``: ctypes binding of ``oracle/build/librans_ref.so`` (oracle/rans_ref.c, the same
   algorithm in C) for full-size byte-exact checks and the CPU coder baseline;
 * ``factorized_tables`` / ``laplace_tables``: restatements of EntropyBottleneck.update() /
@@ -62,6 +65,34 @@ def pmf_to_quantized_cdf_py(pmf, precision=PREC):
                 for j in range(i + 1, best_steal + 1):
                     cdf[j] += 1
     return np.asarray(cdf, np.uint32)
+
+
+def pmf_to_quantized_cdf_np(pmf, precision=PREC):
+    """The same spec (ops.cpp pmf_to_quantized_cdf) restated on the frequency array with numpy,
+    fast enough for every real table (Laplace tables reach 10,611 bins with ~7,800 empty ones).
+    An empty bin's repair changes exactly two frequencies (freq[i] += 1, freq[donor] -= 1; see
+    oracle/rans_ref.c), so no cumulative-table edits are needed."""
+    p = np.asarray(pmf, np.float32)
+    if p.size == 0 or np.any(~(p >= 0)) or not np.all(np.isfinite(p)):
+        raise ValueError("invalid pmf")
+    one = 1 << precision
+    v = (p * np.float32(one)).astype(np.float64)           # float32 product, exact in float64
+    freq = np.floor(v + 0.5).astype(np.int64)              # std::round (v >= 0)
+    total = int(freq.sum())
+    if total == 0:
+        raise ValueError("pmf sums to zero")
+    freq = (one * freq) // total
+    freq[-1] += one - int(freq.sum())
+    for i in np.flatnonzero(freq == 0):                     # bins are repaired in index order
+        if freq[i] != 0:
+            continue
+        cand = np.where(freq > 1, freq, np.iinfo(np.int64).max)
+        donor = int(np.argmin(cand))                        # first minimum = ops.cpp's strict <
+        if freq[donor] <= 1:
+            raise ValueError("no bin to steal from")
+        freq[donor] -= 1
+        freq[i] += 1
+    return np.concatenate([[0], np.cumsum(freq)]).astype(np.uint32)
 
 
 def _push_symbols(symbols, indexes, cdfs, sizes, offsets):
@@ -221,12 +252,15 @@ class CRef:
 
 
 # ------------------------------------------------------------------ table restatements
-def _pack(pmfs, tails, lengths):
+def _pack(pmfs, tails, lengths, quantize=None):
+    """EntropyModel._pmf_to_cdf; quantize defaults to the numpy restatement (the C one is
+    compared against it in tests)."""
+    quantize = quantize or pmf_to_quantized_cdf_np
     max_len = int(max(lengths))
     cdf = np.zeros((len(lengths), max_len + 2), np.int32)
     for i, (p, t, n) in enumerate(zip(pmfs, tails, lengths)):
         prob = np.append(np.asarray(p[:n], np.float64), t).astype(np.float32)
-        q = CRef.pmf_to_quantized_cdf(prob)
+        q = quantize(prob)
         cdf[i, : q.size] = q
     return cdf
 
@@ -244,7 +278,7 @@ def _sig(v):
     return 0.5 * (1.0 + np.tanh(0.5 * v))
 
 
-def factorized_tables(params, tail_mass=1e-9, max_half=150):
+def factorized_tables(params, tail_mass=1e-9, max_half=150, quantize=None):
     """EntropyBottleneck.update() with the BitEstimator CDF and medians fixed at 0."""
     prm = np.asarray(params, np.float32)
     C = prm.shape[1]
@@ -265,10 +299,10 @@ def factorized_tables(params, tail_mass=1e-9, max_half=150):
     sign = -np.sign(lower + upper)
     pmf = np.abs(_sig(sign * upper) - _sig(sign * lower))
     tails = [_sig(lower[c, 0]) + _sig(-upper[c, lengths[c] - 1]) for c in range(C)]
-    return _pack(pmf, tails, lengths), (lengths + 2).astype(np.int32), (-minima).astype(np.int32)
+    return _pack(pmf, tails, lengths, quantize), (lengths + 2).astype(np.int32), (-minima).astype(np.int32)
 
 
-def laplace_tables(scale_table, tail_mass=1e-9):
+def laplace_tables(scale_table, tail_mass=1e-9, quantize=None):
     """GaussianConditional.update() with the Laplace CDF (multiplier -ln(tail_mass))."""
     st = np.asarray(scale_table, np.float32).astype(np.float64)
     center = np.ceil(st * -math.log(tail_mass)).astype(np.int64)
@@ -277,7 +311,8 @@ def laplace_tables(scale_table, tail_mass=1e-9):
     cdf = lambda v: 0.5 - 0.5 * np.sign(v) * np.expm1(-np.abs(v))
     upper = cdf((0.5 - samples) / st[:, None])
     lower = cdf((-0.5 - samples) / st[:, None])
-    return _pack(upper - lower, 2 * lower[:, 0], lengths), (lengths + 2).astype(np.int32), (-center).astype(np.int32)
+    return (_pack(upper - lower, 2 * lower[:, 0], lengths, quantize), (lengths + 2).astype(np.int32),
+            (-center).astype(np.int32))
 
 
 def build_indexes(scales, scale_table):
@@ -287,3 +322,22 @@ def build_indexes(scales, scale_table):
     for t in np.asarray(scale_table, np.float32)[:-1]:
         idx -= (s <= t).astype(np.int32)
     return idx
+
+
+def gaussian_tables(scale_table, tail_mass=1e-9, quantize=None):
+    """compressai GaussianConditional.update() (the table build RLVC's RecProbModel runs through
+    update_scale_table, entropy_models.py:43-48). compressai evaluates the pmf with float32 torch
+    ops (Phi(x) = 0.5 * erfc(-x / sqrt(2))), so this restatement does too; the multiplier is
+    -Phi^-1(tail_mass / 2) (scipy.stats.norm.ppf, as compressai's _standardized_quantile)."""
+    import scipy.stats
+    import torch
+    st = torch.as_tensor(np.asarray(scale_table, np.float32))
+    mult = -float(scipy.stats.norm.ppf(tail_mass / 2))
+    center = torch.ceil(st * mult).int()
+    lengths = (2 * center + 1).numpy().astype(np.int64)
+    samples = torch.abs(torch.arange(int(lengths.max())).int() - center[:, None]).float()
+    phi = lambda v: 0.5 * torch.erfc(v * -(2 ** -0.5))
+    upper = phi((0.5 - samples) / st[:, None])
+    lower = phi((-0.5 - samples) / st[:, None])
+    return (_pack((upper - lower).numpy(), (2 * lower[:, 0]).numpy(), lengths, quantize),
+            (lengths + 2).astype(np.int32), (-center.numpy()).astype(np.int32))

@@ -11,6 +11,14 @@
  * Reference call sites: entropy_models.py:80-94 (RecProbModel.compress/decompress).
  * Written the way compressai structures it (forward push into a symbol queue, then a
  * reverse flush) so it independently checks the device kernel's reverse walk.
+ *
+ * Independence from the product: the product's host quantiser (fvc_coder.hip,
+ * fvc_pmf_to_quantized_cdf) follows ops.cpp literally, editing the cumulative table in place.
+ * This one works on the per-bin frequency array instead. ops.cpp's repair of an empty bin i
+ * ("steal one count from the lowest bin j with freq > 1": cdf[j+1..i] -= 1 if j < i, else
+ * cdf[i+1..j] += 1) changes exactly two frequencies, freq[i] += 1 and freq[j] -= 1, so the
+ * repair loop below is a different program with the same output by construction; the two are
+ * compared table for table in tests/test_coder_oracle.py.
  */
 #include <math.h>
 #include <stdint.h>
@@ -22,31 +30,48 @@
 #define MAX_BYPASS ((1 << BYPASS_PREC) - 1)
 #define RANS64_L (1ull << 31)
 
+/* half away from zero, as std::round on the float product */
+static uint32_t round_half_away(float v) {
+  const double d = (double)v;
+  return (uint32_t)(d >= 0 ? floor(d + 0.5) : -floor(-d + 0.5));
+}
+
 int ref_pmf_to_quantized_cdf(const float *pmf, int n, int precision, uint32_t *cdf) {
-  for (int i = 0; i < n; ++i)
-    if (pmf[i] < 0 || !isfinite(pmf[i])) return -1;
-  cdf[0] = 0;
-  for (int i = 0; i < n; ++i) cdf[i + 1] = (uint32_t)roundf(pmf[i] * (float)(1 << precision));
-  int total_i = 0;
-  for (int i = 0; i <= n; ++i) total_i += (int)cdf[i];
-  uint32_t total = (uint32_t)total_i;
-  if (total == 0) return -1;
-  for (int i = 0; i <= n; ++i) cdf[i] = (uint32_t)(((uint64_t)(1u << precision) * cdf[i]) / total);
-  for (int i = 1; i <= n; ++i) cdf[i] += cdf[i - 1];
-  cdf[n] = 1u << precision;
+  if (n <= 0) return -1;
+  const uint64_t one = 1ull << precision;
+  uint64_t *freq = (uint64_t *)malloc(sizeof(uint64_t) * (size_t)n);
+  if (!freq) return -1;
+  /* 1. scaled, rounded probabilities (float product, as ops.cpp multiplies floats) */
+  uint64_t total = 0;
   for (int i = 0; i < n; ++i) {
-    if (cdf[i] == cdf[i + 1]) {
-      uint32_t best_freq = ~0u;
-      int best_steal = -1;
-      for (int j = 0; j < n; ++j) {
-        uint32_t f = cdf[j + 1] - cdf[j];
-        if (f > 1 && f < best_freq) { best_freq = f; best_steal = j; }
-      }
-      if (best_steal < 0) return -1;
-      if (best_steal < i) { for (int j = best_steal + 1; j <= i; ++j) cdf[j]--; }
-      else { for (int j = i + 1; j <= best_steal; ++j) cdf[j]++; }
-    }
+    if (!(pmf[i] >= 0) || !isfinite(pmf[i])) { free(freq); return -1; }
+    freq[i] = round_half_away(pmf[i] * (float)one);
+    total += freq[i];
   }
+  if (total == 0 || total > 0x7fffffffull) { free(freq); return -1; }
+  /* 2. renormalise each bin by integer division; the last bin absorbs what the floors lost
+   *    (ops.cpp forces the final cumulative value to 2^precision) */
+  uint64_t run = 0;
+  for (int i = 0; i < n; ++i) {
+    freq[i] = (one * freq[i]) / total;
+    run += freq[i];
+  }
+  if (run > one) { free(freq); return -1; }
+  freq[n - 1] += one - run;
+  /* 3. give every empty bin one count, taken from the first smallest bin with more than one */
+  for (int i = 0; i < n; ++i) {
+    if (freq[i] != 0) continue;
+    int donor = -1;
+    for (int j = 0; j < n; ++j)
+      if (freq[j] > 1 && (donor < 0 || freq[j] < freq[donor])) donor = j;
+    if (donor < 0) { free(freq); return -1; }
+    freq[donor] -= 1;
+    freq[i] += 1;
+  }
+  /* 4. cumulative table */
+  cdf[0] = 0;
+  for (int i = 0; i < n; ++i) cdf[i + 1] = cdf[i] + (uint32_t)freq[i];
+  free(freq);
   return 0;
 }
 

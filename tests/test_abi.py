@@ -110,3 +110,36 @@ def test_x3_rejects_unsupported_layers():
     assert lib.fvc_conv_x3_supported(16, 2, 7, 1, 0) == 0   # 7x7 cout <= 4: VALU small-N kernel
     assert lib.fvc_conv_x3_wpack_bytes(16, 2, 7, 1, 0) == 0
     assert lib.fvc_conv_x3_supported(64, 3, 3, 1, 0) == 1   # 3x3 cout <= 4: N padded to one MFMA tile
+
+
+def test_checkpoint_loading_semantics(tmp_path, seeded_sd):
+    """DVC/net.py:21-34 load_model: unknown keys are dropped, a missing file raises; seeded
+    weights are flagged."""
+    import warnings
+    from fastvideocodec_amd.models import SeededWeightsWarning, get_DVC_pretrained
+    with pytest.raises(FileNotFoundError):
+        get_DVC_pretrained(2, checkpoint=str(tmp_path / "nope.model"), device=torch.device("cpu"))
+    sd = dict(seeded_sd)
+    sd["imageCompressor.extra"] = torch.zeros(3)
+    sd["mvEncoder.conv1.bias"] = torch.full_like(sd["mvEncoder.conv1.bias"], 0.5)
+    path = tmp_path / "1024.model"
+    torch.save(sd, path)
+    with warnings.catch_warnings(record=True):
+        warnings.simplefilter("always")
+        m = get_DVC_pretrained(2, checkpoint=str(path), device=torch.device("cpu"))
+    assert m.dropped_checkpoint_keys == ["imageCompressor.extra"] and m.weights_source == str(path)
+    assert float(m.mvEncoder.conv1.bias[0]) == 0.5
+    with pytest.warns(SeededWeightsWarning):
+        m2 = get_DVC_pretrained(2, device=torch.device("cpu"))
+    assert m2.weights_source == "seeded"
+
+
+def test_bench_bookkeeping():
+    import bench
+    e, d = bench.tflop_per_pframe(1088, 1920)
+    assert abs(e + d - 4.226) < 1e-9
+    e4, d4 = bench.tflop_per_pframe(2176, 3840)
+    assert abs((e4 + d4) / (e + d) - 4.0) < 1e-12
+    assert bench.metric_name(1080, 1920) == "1080p frames/sec encode+decode at λ=1024; bpp/PSNR parity vs CPU ref"
+    assert bench.metric_name(2160, 3840).startswith("3840x2160 ")
+    assert 1 <= bench.cpu_cores() <= len(os.sched_getaffinity(0))

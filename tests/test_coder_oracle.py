@@ -1,6 +1,10 @@
 """CPU: the entropy-coder restatements. compressai is absent, so the coder
 is pinned by hand-worked known answers, Python == C byte equality, product-table == oracle-table
-equality and round trips (parity vs compressai itself is unpinned)."""
+equality and round trips (parity vs compressai itself is unpinned).
+
+The product's quantiser (fvc_pmf_to_quantized_cdf, host C++ in libfvc) edits the cumulative
+table in place as ops.cpp does; the oracle's numpy and C quantisers work on the frequency array
+(oracle/rans_ref.c header), so table equality here compares two different programs."""
 import numpy as np
 import pytest
 
@@ -42,17 +46,40 @@ def lap():
     return EM.LaplaceTables()
 
 
-def test_tables_product_equals_oracle(seeded_sd, lap):
-    c, l, o = R.laplace_tables(lap.scale_table)
+@pytest.mark.parametrize("quantizer", ["numpy", "c"])
+def test_tables_product_equals_oracle(seeded_sd, lap, quantizer):
+    """Every real table (64 Laplace scales, 64 z channels, 128 mv channels) built by the product
+    equals the oracle's, with the oracle quantising by its numpy or its C restatement."""
+    q = R.pmf_to_quantized_cdf_np if quantizer == "numpy" else R.CRef.pmf_to_quantized_cdf
+    c, l, o = R.laplace_tables(lap.scale_table, quantize=q)
     assert (c == lap.cdf).all() and (l == lap.cdf_length).all() and (o == lap.offset).all()
+    assert c.shape[0] == 64
     for name, ch in (("bitEstimator_z", 64), ("bitEstimator_mv", 128)):
         rows = [seeded_sd[f"{name}.f{f}.{p}"].numpy().reshape(-1) for f in (1, 2, 3) for p in "hba"]
         rows += [seeded_sd[f"{name}.f4.h"].numpy().reshape(-1), seeded_sd[f"{name}.f4.b"].numpy().reshape(-1)]
         prm = np.stack(rows)
         ft = EM.FactorizedTables(prm)
-        c, l, o = R.factorized_tables(prm)
+        c, l, o = R.factorized_tables(prm, quantize=q)
         assert (c == ft.cdf).all() and (l == ft.cdf_length).all() and (o == ft.offset).all()
         assert ft.cdf.shape[0] == ch
+
+
+def test_quantizers_agree_on_random_pmfs():
+    """Loop restatement (ops.cpp literally) == numpy (frequency array) == C oracle == product, on
+    pmfs with empty bins, ties and heavy tails (the repair path)."""
+    rng = np.random.default_rng(1)
+    for _ in range(300):
+        n = int(rng.integers(1, 60))
+        p = rng.random(n) ** int(rng.integers(1, 30))
+        p[rng.random(n) < 0.3] = 0
+        if p.sum() == 0:
+            p[0] = 1
+        p = (p / p.sum()).astype(np.float32)
+        a = R.pmf_to_quantized_cdf_py(p)
+        b = R.pmf_to_quantized_cdf_np(p)
+        c = R.CRef.pmf_to_quantized_cdf(p)
+        d = EM.pmf_to_quantized_cdf(p)
+        assert a.tolist() == b.tolist() == c.tolist() == d.tolist(), p
 
 
 def test_tables_are_valid_cdfs(lap):
@@ -94,3 +121,11 @@ def test_extreme_escapes(lap):
     idx = np.array([0, 63, 0, 31, 5, 9], np.int32)
     b = R.CRef.encode(sym, idx, lap.cdf, lap.cdf_length, lap.offset)
     assert (R.CRef.decode(b, idx, lap.cdf, lap.cdf_length, lap.offset) == sym).all()
+
+
+def test_gaussian_tables_product_equals_oracle():
+    """compressai GaussianConditional tables (RLVC's RPM path) over get_scale_table()."""
+    g = EM.GaussianTables()
+    c, l, o = R.gaussian_tables(EM.get_scale_table().numpy())
+    assert (c == g.cdf).all() and (l == g.cdf_length).all() and (o == g.offset).all()
+    assert g.cdf_length[0] == 5 and g.offset[0] == -1  # scale 0.11: centre ceil(0.11 * 6.109) = 1

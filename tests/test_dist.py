@@ -29,11 +29,13 @@ def _worker(rank, world, port, q):
         st = fd.gather_stats([rank, len(mine), 10.0 * rank])
         rng = np.random.default_rng(rank)
         payload = rng.integers(0, 256, 1000 + 37 * rank, dtype=np.uint8).tobytes()
-        got = fd.gather_bytes(payload)
+        got = fd.gather_bytes(payload)  # to rank 0 only
         empty = fd.gather_bytes(b"" if rank == 0 else b"x")
-        q.put((rank, mine, t, st.tolist(), [len(g) for g in got], got[1 - rank] ==
-               np.random.default_rng(1 - rank).integers(0, 256, 1000 + 37 * (1 - rank), dtype=np.uint8).tobytes(),
-               empty))
+        if rank == 0:
+            ok = got[1] == np.random.default_rng(1).integers(0, 256, 1037, dtype=np.uint8).tobytes()
+            q.put((rank, mine, t, st.tolist(), [len(g) for g in got], ok, empty))
+        else:
+            q.put((rank, mine, t, st.tolist(), got, True, empty))
     finally:
         dist.destroy_process_group()
 
@@ -53,8 +55,9 @@ def test_gop_sharding_and_gather_gloo_ws2():
     assert sorted(s0 + s1) == list(range(7)) and not set(s0) & set(s1)   # every GOP exactly once
     assert t0 == t1 == 2.0                                               # max over ranks
     assert st0 == st1 == [[0, 4, 0.0], [1, 3, 10.0]]
-    assert l0 == l1 == [1000, 1037] and ok0 and ok1
-    assert e0 == e1 == [b"", b"x"]
+    assert l0 == [1000, 1037] and ok0 and ok1
+    assert l1 is None and e1 is None          # only rank 0 receives the bitstreams
+    assert e0 == [b"", b"x"]
 
 
 def test_single_process_fallbacks():

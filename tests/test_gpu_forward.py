@@ -39,12 +39,16 @@ def test_forward_vs_golden(model, dev, size):
     ref = torch.from_numpy(g["referframe"]).to(dev)
     out, t = model(cur, ref, return_intermediates=True)
     torch.cuda.synchronize()
+    measured = {}
     for name, c in STAGES.items():
         got = nhwc_to_nchw(t[name], c).numpy()
         exp = g[GOLD_NAME.get(name, name)]
         scale = np.abs(exp).max() + 1e-6
         err = np.abs(got - exp).max()
+        measured[name] = float(err / scale)
         assert err <= TOL_TENSOR * scale, f"{name}: {err:.3e} vs {scale:.3e}"
+    measured["clipped_abs"] = float(np.abs(out[0].cpu().numpy() - g["clipped"]).max())
+    print(f"golden {size} max rel dev per stage:", measured)
     for name, gname in (("mvfeature", "quant_mv"), ("feature", "compressed_feature"), ("z", "compressed_z")):
         got = np.round(nhwc_to_nchw(t[name], STAGES[name]).numpy())
         flips = float((got != g[gname]).mean())
@@ -222,25 +226,21 @@ def test_gop_pipeline_bitexact(model, dev):
         assert a.mv.to_bytes_list() == b.mv.to_bytes_list()
 
 
-def test_forward_vs_oracle_1080p(model, dev):
-    """BASELINE.json's full size (1920x1080, replicate-padded to 1088): one synthetic P-frame
-    through the HIP forward and through the CPU oracle (golden-pinned restatement of net.py:70-220)
-    with the same weights. The reference itself is not bit-reproducible across CPU backends at
-    this size, so the bar is the tier's: symbol flip rate <= 1e-3 per latent, PSNR
-    within 1e-3 dB, bpp within 1e-3 relative, stage tensors within 2e-4 of their max-abs."""
-    from fastvideocodec_amd.synthetic import make_gop, gop_seed
-    from fastvideocodec_amd.weights import seeded_torch_state_dict
-    frames = make_gop(1080, 1920, 2, gop_seed(7))
-    cur, ref = torch.from_numpy(frames[1:2].copy()), torch.from_numpy(frames[0:1].copy())
+def _parity_1080p_report(model, dev, cur, ref, inter, o_mse, o_bpp):
+    """Symbol flip rates per latent, stage deviations, dPSNR and bpp deviation of one HIP forward
+    against the oracle's intermediates."""
     out, t = model(cur.to(dev), ref.to(dev), return_intermediates=True)
     torch.cuda.synchronize()
-    torch.set_num_threads(min(16, len(os.sched_getaffinity(0))))
-    (o_clip, o_mse, _, _, o_bf, o_bz, o_bmv, o_bpp), inter = dvc_ref.forward(
-        seeded_torch_state_dict(), cur, ref, return_intermediates=True)
     report = {}
+    nflip = ntot = 0
     for name, gname in (("mvfeature", "quant_mv"), ("feature", "compressed_feature"), ("z", "compressed_z")):
         got = np.round(nhwc_to_nchw(t[name], STAGES[name]).numpy())
-        report[gname] = float((got != inter[gname].numpy()).mean())
+        d = got != inter[gname].numpy()
+        report[gname] = float(d.mean())
+        nflip += int(d.sum())
+        ntot += d.size
+    report["flip_rate_all"] = nflip / ntot
+    report["flips"] = nflip
     for name in ("estmv", "warpframe", "prediction"):
         got = nhwc_to_nchw(t[name], STAGES[name]).numpy()
         exp = inter[name].numpy()
@@ -251,17 +251,60 @@ def test_forward_vs_oracle_1080p(model, dev):
     psnr_exp = 10 * np.log10(1.0 / float(o_mse))
     report["dpsnr_db"] = abs(psnr_got - psnr_exp)
     report["bpp_rel"] = abs(float(out[7]) - float(o_bpp)) / float(o_bpp)
-    print("1080p parity:", report)
-    for gname in ("quant_mv", "compressed_feature", "compressed_z"):
-        assert report[gname] <= TOL_SYMBOL_FLIP, report
+    return report
+
+
+@pytest.fixture(scope="module")
+def oracle_1080p():
+    from fastvideocodec_amd.synthetic import make_gop, gop_seed
+    from fastvideocodec_amd.weights import seeded_torch_state_dict
+    frames = make_gop(1080, 1920, 2, gop_seed(7))
+    cur, ref = torch.from_numpy(frames[1:2].copy()), torch.from_numpy(frames[0:1].copy())
+    torch.set_num_threads(min(16, len(os.sched_getaffinity(0))))
+    (o_clip, o_mse, _, _, o_bf, o_bz, o_bmv, o_bpp), inter = dvc_ref.forward(
+        seeded_torch_state_dict(), cur, ref, return_intermediates=True)
+    return cur, ref, inter, o_mse, o_bpp
+
+
+# T3 at BASELINE's full size: the reference itself flips 3 mv / 24 feature / 2 z of
+# 1.86 M symbols between two CPU backends (aggregate 1.56e-5); the HIP path must stay inside that
+# and inside the north star's 1e-4 dB. Per-latent bounds sit ~3x above the measured rates (r1, MI355X:
+# mv 1.7e-5, feature 1.3e-6, z 0), so a regression to fp16-level accuracy (flip rates ~1e-3) fails.
+TOL_1080P_FLIPS_ALL = 1.56e-5
+TOL_1080P_FLIPS = {"quant_mv": 5e-5, "compressed_feature": 5e-6, "compressed_z": 3.1e-5}
+
+
+def test_forward_vs_oracle_1080p(model, dev, oracle_1080p):
+    """BASELINE.json's full size (1920x1080, replicate-padded to 1088): one synthetic P-frame
+    through the HIP forward (default split-precision convs) and through the CPU oracle
+    (golden-pinned restatement of net.py:70-220) with the same weights."""
+    cur, ref, inter, o_mse, o_bpp = oracle_1080p
+    report = _parity_1080p_report(model, dev, cur, ref, inter, o_mse, o_bpp)
+    print("1080p parity (x3):", report)
+    assert report["flip_rate_all"] <= TOL_1080P_FLIPS_ALL, report
+    for gname, tol in TOL_1080P_FLIPS.items():
+        assert report[gname] <= tol, (gname, report)
     for name in ("estmv", "warpframe", "prediction"):
         # mean deviation at the small-size tier; the max is a few isolated pixels where SpyNet's
         # warp-and-refine iterations amplify ulp-level differences (the reference itself moves
-        # there between CPU backends)
-        assert report[name + "_mean"] <= TOL_TENSOR * 0.1, report
+        # there between CPU backends, SURVEY §7) or a flipped MV symbol moves the warp
+        assert report[name + "_mean"] <= 2e-6, report
         assert report[name] <= 1e-2, report
-    assert report["dpsnr_db"] <= 1e-3, report
-    assert report["bpp_rel"] <= 1e-3, report
+    assert report["dpsnr_db"] <= TOL_PSNR_DB, report
+    assert report["bpp_rel"] <= 1e-5, report
+
+
+def test_forward_x3_vs_f32_1080p(model, dev, oracle_1080p):
+    """The split-precision convs add no symbol flips beyond fp32 noise: the same 1080p frame run
+    on the fp32-MFMA kernels flips about as many symbols against the oracle as the x3 path."""
+    from fastvideocodec_amd import kernels as K
+    cur, ref, inter, o_mse, o_bpp = oracle_1080p
+    r3 = _parity_1080p_report(model, dev, cur, ref, inter, o_mse, o_bpp)
+    with K.precision("f32"):
+        r32 = _parity_1080p_report(model, dev, cur, ref, inter, o_mse, o_bpp)
+    print("1080p flips x3:", r3["flips"], "f32:", r32["flips"], r32)
+    assert r32["dpsnr_db"] <= TOL_PSNR_DB
+    assert r3["flips"] <= 2 * r32["flips"] + 10, (r3, r32)
 
 
 def test_gop_streaming_back_to_back(model, dev):
