@@ -21,8 +21,8 @@ def _hipcc():
     return os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 
-def _obj(src):
-    return os.path.join(OBJDIR, os.path.splitext(src)[0] + ".o")
+def _obj(src, tag=""):
+    return os.path.join(OBJDIR, os.path.splitext(src)[0] + tag + ".o")
 
 
 def _stale(target, deps):
@@ -32,31 +32,42 @@ def _stale(target, deps):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def _compile(src, verbose):
+def _compile(src, verbose, extra=(), tag=""):
     path = os.path.join(HERE, "csrc", src)
-    obj = _obj(src)
-    cmd = [_hipcc()] + FLAGS + ["-c", path, "-o", obj + ".tmp"]
+    obj = _obj(src, tag)
+    cmd = [_hipcc()] + FLAGS + list(extra) + ["-c", path, "-o", obj + ".tmp"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
     os.replace(obj + ".tmp", obj)
 
 
-def build(force=False, verbose=True):
+def build(force=False, verbose=True, variant=None, defines=()):
+    """Build libfvc.so; variant="name" with extra -D defines builds an experiment library
+    libfvc_<name>.so instead (loaded with FVC_LIB_PATH; never the product)."""
     os.makedirs(OBJDIR, exist_ok=True)
-    todo = [s for s in SRCS if force or _stale(_obj(s), [os.path.join(HERE, "csrc", s)] + HEADERS)]
+    tag = f"_{variant}" if variant else ""
+    out = OUT if not variant else os.path.join(HERE, f"libfvc{tag}.so")
+    extra = [f"-D{d}" for d in defines]
+    todo = [s for s in SRCS if force or _stale(_obj(s, tag), [os.path.join(HERE, "csrc", s)] + HEADERS)]
     if todo:
         with ThreadPoolExecutor(max_workers=min(len(todo), 4)) as ex:
-            list(ex.map(lambda s: _compile(s, verbose), todo))
-    objs = [_obj(s) for s in SRCS]
-    if force or todo or _stale(OUT, objs):
-        cmd = [_hipcc(), "--offload-arch=gfx950", "-shared", "-fPIC", "-o", OUT + ".tmp"] + objs
+            list(ex.map(lambda s: _compile(s, verbose, extra, tag), todo))
+    objs = [_obj(s, tag) for s in SRCS]
+    if force or todo or _stale(out, objs):
+        cmd = [_hipcc(), "--offload-arch=gfx950", "-shared", "-fPIC", "-o", out + ".tmp"] + objs
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         subprocess.run(cmd, check=True)
-        os.replace(OUT + ".tmp", OUT)
-    return OUT
+        os.replace(out + ".tmp", out)
+    return out
 
 
 if __name__ == "__main__":
-    build(force="--force" in sys.argv)
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("--variant", default=None)
+    ap.add_argument("-D", dest="defines", action="append", default=[])
+    a = ap.parse_args()
+    build(force=a.force, variant=a.variant, defines=a.defines)

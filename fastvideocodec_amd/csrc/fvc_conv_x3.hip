@@ -47,18 +47,20 @@ typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 
 constexpr int kMaxTapsX = 49;
 
-// Accumulation scheme. Dual (default): two weight planes (hi, lo*2^11); the correction
-// products go to a second accumulator scaled by 2^-11 at the end. Single (-DFVC_X3_SINGLE,
-// experiment): three planes, hi, lo (unscaled: w*2^kw keeps it in fp16's normal range) and
-// hi*2^-11, all products in ONE accumulator (acc += xh*wh + xh*wl + xl_s*(wh*2^-11)), which
-// frees 64 VGPRs for a distance-2 operand prefetch. Measured (scripts/conv_micro.py, MI355X):
-// single is 8-13 % slower -- the 50 % larger weight stream costs more than the deeper prefetch
-// gains -- so dual ships.
-#ifdef FVC_X3_SINGLE
+// Accumulation scheme. Dual (default): two weight planes (hi, lo*2^11) and activations split as
+// hi + lo*2^-11; the correction products go to a second accumulator scaled by 2^-11 at the end.
+// Fused (-DFVC_X3_FUSED, experiment): the residual halves are kept UNSCALED, v = hi + lo with
+// lo = fp16(v - hi) (weights are pre-scaled by 2^kw, so their residuals stay normal fp16; an
+// activation's residual below 2^-14 is an fp16 subnormal, an absolute error <= 2^-25 per
+// element), and all three products go to ONE accumulator (acc += wh*xh + wl*xh + wh*xl):
+// the same two weight planes, half the accumulator registers (64 fewer VGPRs at WM = WN = 2),
+// which pays for a distance-2 operand prefetch. The accumulation rounds like an fp32 conv.
+#ifdef FVC_X3_FUSED
 constexpr bool kSingleAcc = true;
 #else
 constexpr bool kSingleAcc = false;
 #endif
+constexpr float kLoScale = kSingleAcc ? 1.f : 2048.f;  // activation residual scale
 // Staged items split between the MFMA tiles of the next half-step (-DFVC_X3_ILV, experiment):
 // measured neutral to 2 % slower than splitting after the MFMAs (scripts/conv_micro.py), so off.
 #ifdef FVC_X3_ILV
@@ -66,7 +68,7 @@ constexpr bool kInterleave = true;
 #else
 constexpr bool kInterleave = false;
 #endif
-constexpr int kNPL = kSingleAcc ? 3 : 2;   // weight planes per (k-step, N-tile)
+constexpr int kNPL = 2;                    // weight planes per (k-step, N-tile): hi, lo
 constexpr int kFrag = 64 * kNPL;          // uint4 per (k-step, N-tile)
 
 struct X3Args {
@@ -115,7 +117,7 @@ __device__ __forceinline__ void split8(const float (&v)[8], h8& hi, h8& lo, floa
     const f2v x = {v[i], v[i + 1]};
     const h2v h = __builtin_convertvector(x, h2v);
     const f2v back = __builtin_convertvector(h, f2v);
-    const h2v l = __builtin_convertvector((x - back) * 2048.f, h2v);
+    const h2v l = __builtin_convertvector((x - back) * kLoScale, h2v);
     hi[i] = h[0];
     hi[i + 1] = h[1];
     lo[i] = l[0];
@@ -256,7 +258,7 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(const X3Args a) {
 
   struct Ops {
     h8 ah[WM], al[WM];
-    uint4 bh[WN], bl[WN], bd[kSingleAcc ? WN : 1];
+    uint4 bh[WN], bl[WN];
   };
   f32x16 acc[WM][WN], cor[WM][kSingleAcc ? 1 : WN];
   int buf = 0;  // LDS buffer holding the chunk being multiplied
@@ -325,11 +327,9 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(const X3Args a) {
           } else if constexpr (DBG & 2) {
             op.bh[n] = make_uint4(q, n, 1, 2);
             op.bl[n] = op.bh[n];
-            if constexpr (kSingleAcc) op.bd[n] = op.bh[n];
           } else {
             op.bh[n] = wk[n * kFrag];
             op.bl[n] = wk[n * kFrag + 64];
-            if constexpr (kSingleAcc) op.bd[n] = wk[n * kFrag + 128];
           }
         }
       };
@@ -342,10 +342,9 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(const X3Args a) {
             // so each lane ends up with 4 consecutive channels of one pixel per register group
             // (16-B epilogue stores)
             if constexpr (kSingleAcc) {
-              const h8 wd = __builtin_bit_cast(h8, op.bd[n]);
               acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wh, op.ah[m], acc[m][n], 0, 0, 0);
               acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wl, op.ah[m], acc[m][n], 0, 0, 0);
-              acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wd, op.al[m], acc[m][n], 0, 0, 0);
+              acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wh, op.al[m], acc[m][n], 0, 0, 0);
             } else {
               acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wh, op.ah[m], acc[m][n], 0, 0, 0);
               cor[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wl, op.ah[m], cor[m][n], 0, 0, 0);
@@ -378,7 +377,7 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(const X3Args a) {
             const f2v x = {x0, x1};
             const h2v h = __builtin_convertvector(x, h2v);
             const f2v back = __builtin_convertvector(h, f2v);
-            const h2v l = __builtin_convertvector((x - back) * 2048.f, h2v);
+            const h2v l = __builtin_convertvector((x - back) * kLoScale, h2v);
             // pin the conversion to this slice (pure arithmetic is otherwise free to sink to the
             // LDS write in instruction selection, where sched_barrier has no say)
             asm volatile("" ::"v"(h), "v"(l));
@@ -1026,7 +1025,6 @@ int fvc_conv_x3_pack_weight(const float* w, void* wp, float* osc_out, int cin, i
               out[frag + e] = hi;  // plane 0 (hi): lanes 0..63
               if (kSingleAcc) {
                 out[frag + 64 * 8 + e] = (_Float16)(v - (float)hi);              // plane 1: lo, unscaled
-                out[frag + 128 * 8 + e] = (_Float16)((float)hi * (1.f / 2048.f));  // plane 2: hi * 2^-11
               } else {
                 out[frag + 64 * 8 + e] = (_Float16)((v - (float)hi) * 2048.f);   // plane 1: lo * 2^11
               }

@@ -40,6 +40,7 @@ CASES = {
 ap = argparse.ArgumentParser()
 ap.add_argument("--cases", default=",".join(CASES))
 ap.add_argument("--iters", type=int, default=10)
+ap.add_argument("--batch", type=int, default=1)
 args = ap.parse_args()
 dev = torch.device("cuda")
 for name in args.cases.split(","):
@@ -49,10 +50,11 @@ for name in args.cases.split(","):
         H, W = H // 2, W // 2
     w = torch.randn((cin, cout, k, k) if tr else (cout, cin, k, k)) * 0.05
     pc = K.PackedConv(w, torch.zeros(cout), k, s, tr, dev)
-    x = torch.randn(1, H, W, K.cp4(cin), device=dev)
+    B = args.batch
+    x = torch.randn(B, H, W, K.cp4(cin), device=dev)
     kw = {}
     if with_res:
-        kw = dict(in_op=K.IN_RELU, res=torch.randn(1, H, W, K.cp4(cout), device=dev))
+        kw = dict(in_op=K.IN_RELU, res=torch.randn(B, *pc.out_hw(H, W), K.cp4(cout), device=dev))
     y = pc(x, **kw)
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -62,5 +64,5 @@ for name in args.cases.split(","):
     e1.record()
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / args.iters
-    fl = conv_flops(cin, cout, k, s, tr, 1, H, W)
+    fl = conv_flops(cin, cout, k, s, tr, B, H, W)
     print(f"{name:16s} {ms:8.3f} ms  {fl / ms / 1e9:8.2f} TF/s", flush=True)

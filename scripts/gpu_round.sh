@@ -4,7 +4,7 @@
 export TMPDIR=/tmp
 TAG=${1:-run}
 mkdir -p gpurun_out
-timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread -p no:cacheprovider \
+timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread -p no:cacheprovider -rP \
   --tb=short > gpurun_out/pytest_gpu_$TAG.log 2>&1
 rc=$?
 echo "pytest exit $rc" >> gpurun_out/pytest_gpu_$TAG.log

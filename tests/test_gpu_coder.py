@@ -158,12 +158,12 @@ def test_rans_encoder_empty_stream_flushes_state(dev):
 
 
 def _overflowing_model(dev, policy):
-    """Seeded weights with Warp_net's last ResBlock's first conv scaled by 3e4: its output (the
+    """Seeded weights with Warp_net's last ResBlock's first conv scaled by 1e7: its output (the
     next conv's input) leaves the split-precision range (|v| >= 65000)."""
     m = get_codec_model("DVC-pretrained", compression_level=2, device=dev)
     with torch.no_grad():
-        m.warpnet.conv5.conv1.weight.mul_(3e4)
-        m.warpnet.conv5.conv1.bias.mul_(3e4)
+        m.warpnet.conv5.conv1.weight.mul_(1e7)
+        m.warpnet.conv5.conv1.bias.mul_(1e7)
     m.invalidate()
     m.on_overflow = policy
     return m

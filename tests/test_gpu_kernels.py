@@ -214,6 +214,28 @@ def test_conv_x3_matches_f32_closely(dev):
     assert e3 <= 4e-6 * scale, (e3, e32, scale)
 
 
+@pytest.mark.parametrize("xscale", [1e-4, 1e-2, 1.0, 3e3])
+def test_conv_x3_accuracy_across_activation_scales(dev, xscale):
+    """The split keeps fp32-level accuracy from tiny activations (residual halves in fp16's
+    subnormal range) to large ones: max error vs a float64 conv within 4e-6 of the output
+    scale, and within 4x the fp32-MFMA kernel's own error."""
+    g = torch.Generator().manual_seed(12)
+    x = (torch.rand(1, 64, 40, 72, generator=g) - 0.3) * xscale
+    w = torch.randn(64, 64, 3, 3, generator=g) * 0.04
+    b = torch.randn(64, generator=g) * 0.1 * xscale
+    ref = F.conv2d(x.double(), w.double(), b.double(), 1, 1)
+    xd = to_nhwc(x).to(dev)
+    y3 = K.PackedConv(w, b, 3, 1, False, dev, precision="x3")(xd)
+    y32 = K.PackedConv(w, b, 3, 1, False, dev, precision="f32")(xd)
+    torch.cuda.synchronize()
+    e3 = float((from_nhwc(y3.cpu(), 64).double() - ref).abs().max())
+    e32 = float((from_nhwc(y32.cpu(), 64).double() - ref).abs().max())
+    scale = float(ref.abs().max())
+    print(f"xscale {xscale}: x3 err {e3 / scale:.2e}, f32 err {e32 / scale:.2e} (relative to output scale)")
+    assert e3 <= 4e-6 * scale, (e3, e32, scale)
+    assert e3 <= 4 * e32 + 1e-7 * scale, (e3, e32, scale)
+
+
 def test_conv_deterministic(dev):
     g = torch.Generator().manual_seed(7)
     x = torch.randn(1, 64, 33, 65, generator=g)
