@@ -47,27 +47,12 @@ typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 
 constexpr int kMaxTapsX = 49;
 
-// Accumulation scheme. Dual (default): two weight planes (hi, lo*2^11) and activations split as
-// hi + lo*2^-11; the correction products go to a second accumulator scaled by 2^-11 at the end.
-// Fused (-DFVC_X3_FUSED, experiment): the residual halves are kept UNSCALED, v = hi + lo with
-// lo = fp16(v - hi) (weights are pre-scaled by 2^kw, so their residuals stay normal fp16; an
-// activation's residual below 2^-14 is an fp16 subnormal, an absolute error <= 2^-25 per
-// element), and all three products go to ONE accumulator (acc += wh*xh + wl*xh + wh*xl):
-// the same two weight planes, half the accumulator registers (64 fewer VGPRs at WM = WN = 2),
-// which pays for a distance-2 operand prefetch. The accumulation rounds like an fp32 conv.
-#ifdef FVC_X3_FUSED
-constexpr bool kSingleAcc = true;
-#else
-constexpr bool kSingleAcc = false;
-#endif
-constexpr float kLoScale = kSingleAcc ? 1.f : 2048.f;  // activation residual scale
-// Staged items split between the MFMA tiles of the next half-step (-DFVC_X3_ILV, experiment):
-// measured neutral to 2 % slower than splitting after the MFMAs (scripts/conv_micro.py), so off.
-#ifdef FVC_X3_ILV
-constexpr bool kInterleave = true;
-#else
-constexpr bool kInterleave = false;
-#endif
+// Accumulation: two weight planes (hi, lo*2^11) and activations split as hi + lo*2^-11; the
+// correction products go to a second accumulator scaled by 2^-11 at the end. (Measured and
+// rejected, r2: one accumulator with UNSCALED residual halves -- 64 fewer VGPRs, same speed on
+// every geometry (scripts/gpu_x3_variants.sh), but an activation residual below 2^-14 is an
+// fp16 subnormal and small-activation layers lose accuracy: 4.8e-4 relative at |x| ~ 1e-4.)
+constexpr float kLoScale = 2048.f;  // activation residual scale
 constexpr int kNPL = 2;                    // weight planes per (k-step, N-tile): hi, lo
 constexpr int kFrag = 64 * kNPL;          // uint4 per (k-step, N-tile)
 
@@ -91,8 +76,8 @@ struct X3Args {
   int oy0[4], ox0[4];
   long long wcls[4];               // uint4 offset of each class in the pack
   int ps;                          // LDS plane stride (halves): 8 x (pixels rounded to 8 mod 16)
-  int bq;                          // BL: uint4 per LDS weight buffer (max k-steps x WN x kFrag)
-  unsigned y_bytes;                // bytes of y (and res): < 4 GB - 256, the buffer range
+  unsigned y_bytes;                // bytes of y (and res): < 4 GB - 4 KB, the buffer range
+  unsigned x_bytes;                // bytes of one input image: < 4 GB - 4 KB
   int* ovf;                        // caller's overflow flag (device int; may be null)
   int toff[4][kMaxTapsX + 1];      // LDS offset (halves) of each tap's window; 0 past ntaps
 };
@@ -127,13 +112,17 @@ __device__ __forceinline__ void split8(const float (&v)[8], h8& hi, h8& lo, floa
                        fmaxf(fmaxf(fabsf(v[4]), fabsf(v[5])), fmaxf(fabsf(v[6]), fabsf(v[7])))));
 }
 
-// DBG (ablation builds only, scripts/gpu_x3_ablate.sh; 0 in the product): bit 0 no staging of
-// later chunks, bit 1 no weight loads in the k-loop, bit 2 no output stores, bit 3 no A LDS reads,
-// bit 4 output stores issued with an out-of-range offset (dropped by the buffer range check)
-template <int CC, int WM, int WN, int NW, int IOP, int BL, int DBG = 0>
-__global__ __launch_bounds__(NW * 64) void conv_x3_kernel(const X3Args a) {
+// x and y / res are addressed through buffer descriptors with 32-bit offsets (the host keeps
+// each image's input and each launch's output under 4 GB): a halo pixel outside the image gets an
+// offset past the descriptor's range and loads zeros (the conv's zero padding, no select), and a
+// store whose lane is outside the output is dropped by the same range check -- no branches.
+constexpr unsigned kOob = 0xFFFFFF00u;
+constexpr int kRsrcFlags = 0x00020000;
+
+template <int CC, int WM, int WN, int IOP, int POST>
+__global__ __launch_bounds__(512) void conv_x3_kernel(const X3Args a) {
+  constexpr int NW = 8;
   constexpr int C8 = CC / 8;
-  static_assert(!(kSingleAcc && BL), "weights-in-LDS path is dual-accumulator only");
   constexpr int TH = NW * WM;
   constexpr int TW = 32;
   constexpr int NT = NW * 64;
@@ -147,8 +136,6 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(const X3Args a) {
   float* const sbias = reinterpret_cast<float*>(smh);
   static_assert(WN * 32 * 4 <= 512, "bias area");
   _Float16* const sdump = smh + 256;  // 32 B sink for staging writes of items past the tile
-  // BL: two weight buffers after the A buffers, each [k-step][N-tile][hi|lo][lane] uint4
-  _Float16* const wlds0 = tile0 + 2 * tile_h;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -174,18 +161,19 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(const X3Args a) {
   const int nch = a.nchunks;
   const int tile_items = a.ir * a.ic * C8;
   const int nstage = (tile_items + NT - 1) / NT;
-  const float* xb = a.x + (size_t)b * a.H * a.W * a.cinp;
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(a.x + (size_t)b * a.H * a.W * a.cinp), (short)0, (int)a.x_bytes, kRsrcFlags);
   const uint4* wcls = a.w + a.wcls[cls];  // (cls, nq, wcls, tap_tab: updated per work item)
   float mx = 0.f;  // max |staged value| (fp16 representability check)
 
-  // one staging item = 8 channels of one halo pixel: 2 x float4 global -> hi/lo h8 in LDS.
-  // fetch always issues its two loads (index and coordinates clamped, halo padding selected to 0
-  // in store), so the k-loop has no divergent branches and the compiler can count vmcnt exactly;
-  // in_op, the split and the LDS write happen in store, after the MFMAs.
+  // one staging item = 8 channels of one halo pixel: 2 x 16-B buffer loads -> hi/lo h8 in LDS.
+  // fetch always issues its two loads (halo pixels outside the image read zeros through the
+  // descriptor's range check), so the k-loop has no divergent branches and the compiler can
+  // count vmcnt exactly; in_op, the split and the LDS write happen in store, after the MFMAs.
   struct Stage {
     float4 v0, v1;
     int dst;
-    bool inb, ok;
+    bool ok;
   };
   auto fetch = [&](int e, int tile, int ch, Stage& st) {
     st.ok = e < tile_items;  // past the end: loads of a clamped index, no LDS write
@@ -196,19 +184,17 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(const X3Args a) {
     const int c = p - r * a.ic;
     const int iy = (tile / tiles_x) * TH * a.sin + a.dymin + r;
     const int ix = (tile % tiles_x) * TW * a.sin + a.dxmin + c;
-    st.inb = iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
-    const int cy = iy < 0 ? 0 : (iy >= a.H ? a.H - 1 : iy);
-    const int cx = ix < 0 ? 0 : (ix >= a.W ? a.W - 1 : ix);
-    const float* src = xb + ((size_t)cy * a.W + cx) * a.cinp + ch * CC + o * 8;
-    st.v0 = *reinterpret_cast<const float4*>(src);
-    st.v1 = *reinterpret_cast<const float4*>(src + 4);
+    const bool inb = (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
+    const unsigned off = inb ? ((unsigned)(iy * a.W + ix) * (unsigned)a.cinp + (unsigned)(ch * CC + o * 8)) * 4u : kOob;
+    st.v0 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rx, off, 0, 0));
+    st.v1 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rx, off + 16u, 0, 0));
     const int cpos = hf ? ((c & 1) * hf + (c >> 1)) : c;
     st.dst = o * a.ps + (r * a.ic + cpos) * 8;  // plane o (hi), pixel-minor
   };
   auto store = [&](_Float16* t, const Stage& st) {
     float v[8] = {st.v0.x, st.v0.y, st.v0.z, st.v0.w, st.v1.x, st.v1.y, st.v1.z, st.v1.w};
 #pragma unroll
-    for (int i = 0; i < 8; ++i) v[i] = st.inb ? in_op_t<IOP>(v[i]) : 0.f;
+    for (int i = 0; i < 8; ++i) v[i] = in_op_t<IOP>(v[i]);  // zero padding stays zero
     h8 hi, lo;
     split8(v, hi, lo, mx);
     // branch-free (keeps the split in the MFMA basic block for interleaving): items past the
@@ -218,31 +204,11 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(const X3Args a) {
     *reinterpret_cast<h8*>(ph) = hi;
     *reinterpret_cast<h8*>(pl) = lo;
   };
-  // BL: one weight staging item = one uint4 of the next chunk's [k-step][N-tile][hi|lo][lane]
-  // block slice (contiguous per k-step: N-tiles nt0..nt0+WN-1 are adjacent in the pack)
-  const int bitems = nq * WN * kFrag;
-  const int nbstage = BL ? (bitems + NT - 1) / NT : 0;
-  auto bfetch = [&](int i, int ch, uint4& v) {
-    i = i < bitems ? i : bitems - 1;
-    const int q = i / (WN * kFrag);
-    const int rem = i - q * (WN * kFrag);
-    v = wcls[((size_t)ch * nq + q) * a.ntp * kFrag + nt0 * kFrag + rem];
-  };
-  auto bstore = [&](_Float16* wb, int i, const uint4& v) {
-    if (i < bitems) *reinterpret_cast<uint4*>(wb + (size_t)i * 8) = v;
-  };
 
   for (int e = tid; e < tile_items; e += NT) {
     Stage st;
     fetch(e, w_begin / a.nclass, 0, st);
     store(tile0, st);
-  }
-  if constexpr (BL != 0) {
-    for (int i = tid; i < bitems; i += NT) {
-      uint4 v;
-      bfetch(i, 0, v);
-      bstore(wlds0, i, v);
-    }
   }
   if (tid < WN * 32) {
     const int j = nt0 * 32 + tid;
@@ -260,8 +226,12 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(const X3Args a) {
     h8 ah[WM], al[WM];
     uint4 bh[WN], bl[WN];
   };
-  f32x16 acc[WM][WN], cor[WM][kSingleAcc ? 1 : WN];
+  f32x16 acc[WM][WN], cor[WM][WN];
   int buf = 0;  // LDS buffer holding the chunk being multiplied
+  const __amdgpu_buffer_rsrc_t ry =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.y, (short)0, (int)a.y_bytes, kRsrcFlags);
+  const __amdgpu_buffer_rsrc_t rr =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.res, (short)0, (int)a.y_bytes, kRsrcFlags);
   for (int w = w_begin; w < w_end; ++w) {
     const int tile = w / a.nclass;
     if (w != w_begin) {
@@ -277,7 +247,7 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(const X3Args a) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           acc[m][n][r] = 0.f;
-          if constexpr (!kSingleAcc) cor[m][n][r] = 0.f;
+          cor[m][n][r] = 0.f;
         }
 
     // K loop over channel chunks. Two operand register sets (ping-pong, no copies). Each
@@ -293,10 +263,8 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(const X3Args a) {
       const int s_item = last ? w + 1 : w;
       const int s_tile = s_item / a.nclass;
       const int s_ch = last ? 0 : ch + 1;
-      const bool stage_next = (DBG & 1) ? false : s_item < w_end;
+      const bool stage_next = s_item < w_end;
       const uint4* wch = wcls + (size_t)ch * nq * a.ntp * kFrag;
-      const _Float16* wcur = wlds0 + buf * (a.bq * 8);
-      _Float16* wnxt = wlds0 + (buf ^ 1) * (a.bq * 8);
       // k-step q: lane half lh takes k8-block kb = 2q + lh = (tap kb / C8, octet kb % C8)
       auto load = [&](int q, Ops& op) {
         int toff;
@@ -309,88 +277,30 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(const X3Args a) {
         }
 #pragma unroll
         for (int m = 0; m < WM; ++m) {
-          if constexpr (DBG & 8) {
-            op.ah[m] = (h8)(_Float16)(toff & 7);
-            op.al[m] = op.ah[m];
-          } else {
-            op.ah[m] = *reinterpret_cast<const h8*>(cur + pix0 + m * pix_m + toff);
-            op.al[m] = *reinterpret_cast<const h8*>(cur + pix0 + m * pix_m + toff + C8 * a.ps);
-          }
+          op.ah[m] = *reinterpret_cast<const h8*>(cur + pix0 + m * pix_m + toff);
+          op.al[m] = *reinterpret_cast<const h8*>(cur + pix0 + m * pix_m + toff + C8 * a.ps);
         }
         const uint4* wk = wch + ((size_t)q * a.ntp + nt0) * kFrag + lane;
-        const uint4* wl = reinterpret_cast<const uint4*>(wcur) + q * (WN * kFrag) + lane;
 #pragma unroll
         for (int n = 0; n < WN; ++n) {
-          if constexpr (BL != 0) {
-            op.bh[n] = wl[n * kFrag];
-            op.bl[n] = wl[n * kFrag + 64];
-          } else if constexpr (DBG & 2) {
-            op.bh[n] = make_uint4(q, n, 1, 2);
-            op.bl[n] = op.bh[n];
-          } else {
-            op.bh[n] = wk[n * kFrag];
-            op.bl[n] = wk[n * kFrag + 64];
-          }
+          op.bh[n] = wk[n * kFrag];
+          op.bl[n] = wk[n * kFrag + 64];
         }
       };
-      auto mfma_tile = [&](const Ops& op, const int m, const int n) {
-        {
-          {
-            const h8 wh = __builtin_bit_cast(h8, op.bh[n]);
-            const h8 wl = __builtin_bit_cast(h8, op.bl[n]);
-            // weights as the A (row) operand, pixels as B: the 32x32 result is channel x pixel,
-            // so each lane ends up with 4 consecutive channels of one pixel per register group
-            // (16-B epilogue stores)
-            if constexpr (kSingleAcc) {
-              acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wh, op.ah[m], acc[m][n], 0, 0, 0);
-              acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wl, op.ah[m], acc[m][n], 0, 0, 0);
-              acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wh, op.al[m], acc[m][n], 0, 0, 0);
-            } else {
-              acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wh, op.ah[m], acc[m][n], 0, 0, 0);
-              cor[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wl, op.ah[m], cor[m][n], 0, 0, 0);
-              cor[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wh, op.al[m], cor[m][n], 0, 0, 0);
-            }
-          }
-        }
-      };
+      // weights as the A (row) operand, pixels as B: the 32x32 result is channel x pixel, so
+      // each lane ends up with 4 consecutive channels of one pixel per register group (16-B
+      // epilogue stores)
       auto mfmas = [&](const Ops& op) {
 #pragma unroll
         for (int m = 0; m < WM; ++m)
 #pragma unroll
-          for (int n = 0; n < WN; ++n) mfma_tile(op, m, n);
-      };
-      // the MFMAs of one half-step with a staged item's split + LDS write cut into WM*WN slices,
-      // one after each (m, n) tile's three MFMAs; sched_barrier keeps every slice in place, so a
-      // wave converts while its own matrix ops run
-      auto mfmas_split = [&](const Ops& op, const Stage& st) {
-        constexpr int NP = WM * WN;
-        constexpr int PER = 8 / NP;
-        float v[8] = {st.v0.x, st.v0.y, st.v0.z, st.v0.w, st.v1.x, st.v1.y, st.v1.z, st.v1.w};
-        h8 hi, lo;
-#pragma unroll
-        for (int t = 0; t < NP; ++t) {
-          mfma_tile(op, t / WN, t % WN);
-#pragma unroll
-          for (int i = t * PER; i < (t + 1) * PER; i += 2) {
-            const float x0 = st.inb ? in_op_t<IOP>(v[i]) : 0.f;
-            const float x1 = st.inb ? in_op_t<IOP>(v[i + 1]) : 0.f;
-            const f2v x = {x0, x1};
-            const h2v h = __builtin_convertvector(x, h2v);
-            const f2v back = __builtin_convertvector(h, f2v);
-            const h2v l = __builtin_convertvector((x - back) * kLoScale, h2v);
-            // pin the conversion to this slice (pure arithmetic is otherwise free to sink to the
-            // LDS write in instruction selection, where sched_barrier has no say)
-            asm volatile("" ::"v"(h), "v"(l));
-            hi[i] = h[0]; hi[i + 1] = h[1];
-            lo[i] = l[0]; lo[i + 1] = l[1];
-            mx = fmaxf(mx, fmaxf(fabsf(x0), fabsf(x1)));
+          for (int n = 0; n < WN; ++n) {
+            const h8 wh = __builtin_bit_cast(h8, op.bh[n]);
+            const h8 wl = __builtin_bit_cast(h8, op.bl[n]);
+            acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wh, op.ah[m], acc[m][n], 0, 0, 0);
+            cor[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wl, op.ah[m], cor[m][n], 0, 0, 0);
+            cor[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wh, op.al[m], cor[m][n], 0, 0, 0);
           }
-          if (t + 1 < NP) __builtin_amdgcn_sched_barrier(0);
-        }
-        _Float16* const ph = st.ok ? nxt + st.dst : sdump;
-        _Float16* const pl = st.ok ? nxt + st.dst + C8 * a.ps : sdump + 8;
-        *reinterpret_cast<h8*>(ph) = hi;
-        *reinterpret_cast<h8*>(pl) = lo;
       };
       auto half_plain = [&](int q, const Ops& use, Ops& nxt_ops) {
         load(q + 1 < nq ? q + 1 : nq - 1, nxt_ops);
@@ -398,171 +308,41 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(const X3Args a) {
         mfmas(use);
         __builtin_amdgcn_sched_barrier(0);
       };
-      auto half_stage = [&](int item, int q, const Ops& use, Ops& nxt_ops) {
-        load(q + 1 < nq ? q + 1 : nq - 1, nxt_ops);
+      int staged = 0;
+      Ops S0, S1;
+      load(0, S0);
+      // staging items of the next chunk are spread evenly over the k-step pairs (one per staged
+      // pair) so their VALU work interleaves with MFMA-only steps instead of bunching up at the
+      // chunk start, where every wave would be VALU-bound at once
+      const int npair = nq >> 1;
+      const int nst = stage_next ? min(nstage, npair) : 0;
+      const int spread = nst ? max(1, npair / nst) : 1;
+      int q = 0;
+      for (; staged < nst; ++staged) {
+        // the staged item's split + LDS write come after the pair's second half-step, so its
+        // loads have two half-steps of MFMAs (both waves of the SIMD) to land behind
+        load(q + 1 < nq ? q + 1 : nq - 1, S1);
         Stage st;
-        fetch(item, s_tile, s_ch, st);
+        fetch(tid + staged * NT, s_tile, s_ch, st);
         __builtin_amdgcn_sched_barrier(0);
-        mfmas(use);
+        mfmas(S0);
+        __builtin_amdgcn_sched_barrier(0);
+        load(q + 2 < nq ? q + 2 : nq - 1, S0);
+        __builtin_amdgcn_sched_barrier(0);
+        mfmas(S1);
         __builtin_amdgcn_sched_barrier(0);
         store(nxt, st);
-      };
-      int staged = 0;
-      if constexpr (BL != 0) {
-        // weights from LDS: the k-loop's only global loads are the staging fetches. One A item
-        // (first half) and one weight item (second half) per staged pair, unconditionally (items
-        // past either count load a clamped index and skip the LDS write: branching between
-        // staged and plain halves instead costs ~80 VGPRs and spills at WM = WN = 2).
-        Ops S0, S1;
-        load(0, S0);
-        const int nA = stage_next ? nstage : 0;
-        const int nB = stage_next ? nbstage : 0;
-        const int npair = nq >> 1;
-        const int nst = min(max(nA, nB), npair);
-        const int spread = nst ? max(1, npair / nst) : 1;
-        int q = 0;
-        // every staged load gets more than one half-step of MFMAs to land behind: the A item
-        // fetched in the first half is written after the second half's MFMAs, the weight item
-        // fetched in the second half after the next staged pair's first half
-        uint4 vb;
-        for (; staged < nst; ++staged) {
-          load(q + 1 < nq ? q + 1 : nq - 1, S1);
-          Stage st;
-          fetch(tid + staged * NT, s_tile, s_ch, st);
-          __builtin_amdgcn_sched_barrier(0);
-          mfmas(S0);
-          __builtin_amdgcn_sched_barrier(0);
-          if (staged > 0) bstore(wnxt, tid + (staged - 1) * NT, vb);
-          load(q + 2 < nq ? q + 2 : nq - 1, S0);
-          uint4 vn;
-          bfetch(tid + staged * NT, s_ch, vn);
-          __builtin_amdgcn_sched_barrier(0);
-          mfmas(S1);
-          __builtin_amdgcn_sched_barrier(0);
-          store(nxt, st);
-          vb = vn;
-          q += 2;
-          for (int r = 1; r < spread; ++r, q += 2) {
-            half_plain(q, S0, S1);
-            half_plain(q + 1, S1, S0);
-          }
-        }
-        for (; q + 1 < nq; q += 2) {
+        q += 2;
+        for (int r = 1; r < spread; ++r, q += 2) {
           half_plain(q, S0, S1);
           half_plain(q + 1, S1, S0);
         }
-        if (nq & 1) mfmas(S0);
-        if (nst > 0) bstore(wnxt, tid + (nst - 1) * NT, vb);
-        for (int qs = staged; qs < nB; ++qs) {
-          uint4 v;
-          bfetch(tid + qs * NT, s_ch, v);
-          bstore(wnxt, tid + qs * NT, v);
-        }
-      } else if constexpr (kSingleAcc) {
-        // prefetch distance 2 (the single accumulator leaves room for three operand sets): step
-        // q multiplies S[q % 3] and loads k-step q+2 into the set step q-1 just finished with
-        auto step_plain = [&](int q, const Ops& use, Ops& nxt_ops) {
-          load(q + 2 < nq ? q + 2 : nq - 1, nxt_ops);
-          __builtin_amdgcn_sched_barrier(0);
-          mfmas(use);
-          __builtin_amdgcn_sched_barrier(0);
-        };
-        auto step_stage = [&](int item, int q, const Ops& use, Ops& nxt_ops) {
-          load(q + 2 < nq ? q + 2 : nq - 1, nxt_ops);
-          Stage st;
-          fetch(item, s_tile, s_ch, st);
-          __builtin_amdgcn_sched_barrier(0);
-          mfmas(use);
-          __builtin_amdgcn_sched_barrier(0);
-          store(nxt, st);
-        };
-        Ops S0, S1, S2;
-        load(0, S0);
-        load(nq > 1 ? 1 : 0, S1);
-        const int ntri = nq / 3;
-        const int nst = stage_next ? min(nstage, ntri) : 0;
-        const int spread = nst ? max(1, ntri / nst) : 1;
-        int q = 0;
-        for (; staged < nst; ++staged) {
-          step_stage(tid + staged * NT, q, S0, S2);
-          step_plain(q + 1, S1, S0);
-          step_plain(q + 2, S2, S1);
-          q += 3;
-          for (int r = 1; r < spread; ++r, q += 3) {
-            step_plain(q, S0, S2);
-            step_plain(q + 1, S1, S0);
-            step_plain(q + 2, S2, S1);
-          }
-        }
-        for (; q + 2 < nq; q += 3) {
-          step_plain(q, S0, S2);
-          step_plain(q + 1, S1, S0);
-          step_plain(q + 2, S2, S1);
-        }
-        if (q < nq) mfmas(S0);
-        if (q + 1 < nq) mfmas(S1);
-      } else {
-        Ops S0, S1;
-        load(0, S0);
-        // staging items of the next chunk are spread evenly over the k-step pairs (one per staged
-        // pair) so their VALU work interleaves with MFMA-only steps instead of bunching up at the
-        // chunk start, where every wave would be VALU-bound at once
-        const int npair = nq >> 1;
-        const int nst = stage_next ? min(nstage, npair) : 0;
-        const int spread = nst ? max(1, npair / nst) : 1;
-        int q = 0;
-        if constexpr (kInterleave) {
-          // item i is fetched in staged pair i and split + written in pair i+1, its VALU work
-          // spread between that half-step's MFMAs (sched_group_barrier), so a wave converts while
-          // its own matrix ops run instead of after them
-          Stage sp;  // fetched in the previous staged pair; none before the first (ok = false)
-          sp.v0 = sp.v1 = make_float4(0.f, 0.f, 0.f, 0.f);
-          sp.dst = 0;
-          sp.inb = sp.ok = false;
-          for (; staged < nst; ++staged) {
-            Stage sn;
-            load(q + 1 < nq ? q + 1 : nq - 1, S1);
-            fetch(tid + staged * NT, s_tile, s_ch, sn);
-            __builtin_amdgcn_sched_barrier(0);
-            mfmas_split(S0, sp);
-            __builtin_amdgcn_sched_barrier(0);
-            sp = sn;
-            half_plain(q + 1, S1, S0);
-            q += 2;
-            for (int r = 1; r < spread; ++r, q += 2) {
-              half_plain(q, S0, S1);
-              half_plain(q + 1, S1, S0);
-            }
-          }
-          store(nxt, sp);
-        } else {
-          for (; staged < nst; ++staged) {
-            // the staged item's split + LDS write come after the pair's second half-step, so
-            // its HBM loads have two half-steps of MFMAs (both waves of the SIMD) to land behind
-            load(q + 1 < nq ? q + 1 : nq - 1, S1);
-            Stage st;
-            fetch(tid + staged * NT, s_tile, s_ch, st);
-            __builtin_amdgcn_sched_barrier(0);
-            mfmas(S0);
-            __builtin_amdgcn_sched_barrier(0);
-            load(q + 2 < nq ? q + 2 : nq - 1, S0);
-            __builtin_amdgcn_sched_barrier(0);
-            mfmas(S1);
-            __builtin_amdgcn_sched_barrier(0);
-            store(nxt, st);
-            q += 2;
-            for (int r = 1; r < spread; ++r, q += 2) {
-              half_plain(q, S0, S1);
-              half_plain(q + 1, S1, S0);
-            }
-          }
-        }
-        for (; q + 1 < nq; q += 2) {
-          half_plain(q, S0, S1);
-          half_plain(q + 1, S1, S0);
-        }
-        if (nq & 1) mfmas(S0);
       }
+      for (; q + 1 < nq; q += 2) {
+        half_plain(q, S0, S1);
+        half_plain(q + 1, S1, S0);
+      }
+      if (nq & 1) mfmas(S0);
       if (stage_next) {
         for (int qs = staged; qs < nstage; ++qs) {
           Stage st;
@@ -578,17 +358,9 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(const X3Args a) {
     // Lane (li, lh) holds pixel qx0 + li of strip m; register group g (r = 4g..4g+3) holds output
     // channels N-tile*32 + 8g + 4lh + {0..3} -> one 16-B store (and residual load) per group.
     // Activation as one max: relu = max(v, 0*v), lrelu = max(v, 0.1*v), none = max(v, 1*v).
+    // Pad channels need no select: their weights and bias are 0 and every residual tensor's pad
+    // channels are 0, so they come out 0 -- except after exp (POST), which selects them to 0.
     const int qy0 = (tile / tiles_x) * TH, qx0 = (tile % tiles_x) * TW;
-    // y and res through buffer descriptors with 32-bit offsets (the host keeps each launch's
-    // output under 4 GB): one offset register per output tile instead of 64-bit addresses, and a
-    // store whose lane is outside the output (past Wq / Hq / coutp) gets an offset past the
-    // descriptor's range, which the hardware drops -- no branches. Residual loads of such lanes
-    // read 0 or unused values.
-    const __amdgpu_buffer_rsrc_t ry =
-        __builtin_amdgcn_make_buffer_rsrc((void*)a.y, (short)0, (int)a.y_bytes, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rr =
-        __builtin_amdgcn_make_buffer_rsrc((void*)a.res, (short)0, (int)a.y_bytes, 0x00020000);
-    constexpr unsigned kOob = 0xFFFFFF00u;
     const bool px_ok = qx0 + li < a.Wq;
     auto voff_of = [&](int m, int n) {
       const unsigned qy = qy0 + wave * WM + m;
@@ -627,28 +399,20 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(const X3Args a) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int r = 4 * g + i;
-          float tv;
-          if constexpr (kSingleAcc) tv = acc[m][n][r] * a.osc + bb[i];
-          else tv = fmaf(cor[m][n][r], a.osc_c, acc[m][n][r] * a.osc) + bb[i];
+          const float tv = fmaf(cor[m][n][r], a.osc_c, fmaf(acc[m][n][r], a.osc, bb[i]));
           v[i] = fmaxf(tv, tv * a.act_slope);
         }
         if (a.res) {
           const float4 q4 = rv[t & 1][g];
           v[0] += q4.x; v[1] += q4.y; v[2] += q4.z; v[3] += q4.w;
         }
-        if (a.post_op == FVC_POST_EXP) {
+        if constexpr (POST == FVC_POST_EXP) {
 #pragma unroll
-          for (int i = 0; i < 4; ++i) v[i] = expf(v[i]);
+          for (int i = 0; i < 4; ++i) v[i] = j0 + i < a.cout ? expf(v[i]) : 0.f;
         }
-#pragma unroll
-        for (int i = 0; i < 4; ++i) v[i] = j0 + i < a.cout ? v[i] : 0.f;  // pad channels = 0
-        const unsigned so = ((DBG & 16) == 0 && row_ok && j0 < a.coutp) ? vo + 32u * g : kOob;
-        if constexpr (DBG & 4) {
-          asm volatile("" ::"v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]), "v"(so));
-        } else {
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, make_float4(v[0], v[1], v[2], v[3])),
-                                                 ry, so, 0, 0);
-        }
+        const unsigned so = (row_ok && j0 < a.coutp) ? vo + 32u * g : kOob;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, make_float4(v[0], v[1], v[2], v[3])),
+                                               ry, so, 0, 0);
       }
     }
   }
@@ -795,73 +559,41 @@ static int x3_kw(const float* w, size_t n) {
   return kw < -100 ? -100 : (kw > 100 ? 100 : kw);
 }
 
-template <int CC, int WM, int WN, int IOP, int BL, int DBG>
-static int x3_launch_d(const X3Args& a, dim3 grid, size_t lds, hipStream_t s) {
+template <int CC, int WM, int WN, int IOP, int POST>
+static int x3_launch(const X3Args& a, dim3 grid, size_t lds, hipStream_t s) {
   if (lds > 64 * 1024)
-    (void)hipFuncSetAttribute((const void*)conv_x3_kernel<CC, WM, WN, 8, IOP, BL, DBG>,
+    (void)hipFuncSetAttribute((const void*)conv_x3_kernel<CC, WM, WN, IOP, POST>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL((conv_x3_kernel<CC, WM, WN, 8, IOP, BL, DBG>), grid, dim3(8 * 64), lds, s, a);
+  hipLaunchKernelGGL((conv_x3_kernel<CC, WM, WN, IOP, POST>), grid, dim3(512), lds, s, a);
   FVC_CHECK_LAUNCH();
   return 0;
 }
 
-#ifdef FVC_X3_ABLATE
-static int x3_dbg() {
-  static int d = -1;
-  if (d < 0) d = env_int("FVC_X3_DBG", 0);
-  return d;
-}
-#endif
-
-template <int CC, int WM, int WN, int IOP, int BL>
-static int x3_launch_t(const X3Args& a, dim3 grid, size_t lds, hipStream_t s) {
-#ifdef FVC_X3_ABLATE
-  if (CC == 16 && WM == 2 && WN == 2 && IOP == 0) {
-    switch (x3_dbg()) {
-      case 1: return x3_launch_d<CC, WM, WN, IOP, BL, 1>(a, grid, lds, s);
-      case 2: return x3_launch_d<CC, WM, WN, IOP, BL, 2>(a, grid, lds, s);
-      case 4: return x3_launch_d<CC, WM, WN, IOP, BL, 4>(a, grid, lds, s);
-      case 8: return x3_launch_d<CC, WM, WN, IOP, BL, 8>(a, grid, lds, s);
-      case 3: return x3_launch_d<CC, WM, WN, IOP, BL, 3>(a, grid, lds, s);
-      case 15: return x3_launch_d<CC, WM, WN, IOP, BL, 15>(a, grid, lds, s);
-      case 11: return x3_launch_d<CC, WM, WN, IOP, BL, 11>(a, grid, lds, s);
-      case 16: return x3_launch_d<CC, WM, WN, IOP, BL, 16>(a, grid, lds, s);
-      default: break;
-    }
-  }
-#endif
-  return x3_launch_d<CC, WM, WN, IOP, BL, 0>(a, grid, lds, s);
-}
-
-template <int CC, int WM, int WN, int BL>
-static int x3_launch_iop(int iop, const X3Args& a, dim3 grid, size_t lds, hipStream_t s) {
+// exp after the epilogue is only ever taken with an untransformed input (Synthesis_prior_net
+// deconv3, synthesis_prior.py:25,57): instantiated for IN_NONE only
+template <int CC, int WM, int WN>
+static int x3_launch_iop(int iop, int post, const X3Args& a, dim3 grid, size_t lds, hipStream_t s) {
+  if (post == FVC_POST_EXP)
+    return iop == FVC_IN_NONE ? x3_launch<CC, WM, WN, FVC_IN_NONE, FVC_POST_EXP>(a, grid, lds, s) : FVC_EINVAL;
   switch (iop) {
-    case FVC_IN_NONE: return x3_launch_t<CC, WM, WN, FVC_IN_NONE, BL>(a, grid, lds, s);
-    case FVC_IN_RELU: return x3_launch_t<CC, WM, WN, FVC_IN_RELU, BL>(a, grid, lds, s);
-    case FVC_IN_ABS: return x3_launch_t<CC, WM, WN, FVC_IN_ABS, BL>(a, grid, lds, s);
-    case FVC_IN_ROUND: return x3_launch_t<CC, WM, WN, FVC_IN_ROUND, BL>(a, grid, lds, s);
+    case FVC_IN_NONE: return x3_launch<CC, WM, WN, FVC_IN_NONE, FVC_POST_NONE>(a, grid, lds, s);
+    case FVC_IN_RELU: return x3_launch<CC, WM, WN, FVC_IN_RELU, FVC_POST_NONE>(a, grid, lds, s);
+    case FVC_IN_ABS: return x3_launch<CC, WM, WN, FVC_IN_ABS, FVC_POST_NONE>(a, grid, lds, s);
+    case FVC_IN_ROUND: return x3_launch<CC, WM, WN, FVC_IN_ROUND, FVC_POST_NONE>(a, grid, lds, s);
   }
   return FVC_EINVAL;
 }
 
-template <int CC, int WM, int WN>
-static int x3_launch_bl(int bl, int iop, const X3Args& a, dim3 grid, size_t lds, hipStream_t s) {
-  if constexpr (!kSingleAcc) {
-    if (bl) return x3_launch_iop<CC, WM, WN, 1>(iop, a, grid, lds, s);
-  }
-  return x3_launch_iop<CC, WM, WN, 0>(iop, a, grid, lds, s);
-}
-
-// instantiated shapes (8 waves, 2 per SIMD, <= 256 registers: scripts/kres.sh): WM, WN in {1, 2},
-// weights from L2 (BL=0) or staged per chunk in LDS (BL=1)
+// instantiated shapes (8 waves, 2 per SIMD, <= 256 registers: scripts/kres.sh): WM, WN in {1, 2}
+// and WM = 1 with WN = 4
 template <int CC>
-static int x3_launch_cc(int wm, int wn, int bl, int iop, const X3Args& a, dim3 grid, size_t lds,
+static int x3_launch_cc(int wm, int wn, int iop, int post, const X3Args& a, dim3 grid, size_t lds,
                         hipStream_t s) {
-  if (wm == 2 && wn == 2) return x3_launch_bl<CC, 2, 2>(bl, iop, a, grid, lds, s);
-  if (wm == 2 && wn == 1) return x3_launch_bl<CC, 2, 1>(bl, iop, a, grid, lds, s);
-  if (wm == 1 && wn == 2) return x3_launch_bl<CC, 1, 2>(bl, iop, a, grid, lds, s);
-  if (wm == 1 && wn == 1) return x3_launch_bl<CC, 1, 1>(bl, iop, a, grid, lds, s);
-  if (wm == 1 && wn == 4) return x3_launch_bl<CC, 1, 4>(bl, iop, a, grid, lds, s);
+  if (wm == 2 && wn == 2) return x3_launch_iop<CC, 2, 2>(iop, post, a, grid, lds, s);
+  if (wm == 2 && wn == 1) return x3_launch_iop<CC, 2, 1>(iop, post, a, grid, lds, s);
+  if (wm == 1 && wn == 2) return x3_launch_iop<CC, 1, 2>(iop, post, a, grid, lds, s);
+  if (wm == 1 && wn == 1) return x3_launch_iop<CC, 1, 1>(iop, post, a, grid, lds, s);
+  if (wm == 1 && wn == 4) return x3_launch_iop<CC, 1, 4>(iop, post, a, grid, lds, s);
   return FVC_EINVAL;
 }
 
@@ -899,6 +631,10 @@ static int run_x3(const float* x, const void* wpack, float osc, const float* bia
                   stride, transposed, in_op, act, post_op, cu_reserve, ovf, s);
   }
   a.y_bytes = (unsigned)ybytes;
+  // the input is addressed per image (blockIdx.z) through a 32-bit-range descriptor too
+  const unsigned long long xbytes = (unsigned long long)h * w * c.cinp * 4ull;
+  if (xbytes >= (1ull << 32) - 4096) return FVC_EINVAL;
+  a.x_bytes = (unsigned)xbytes;
   a.ovf = ovf;
   a.sin = c.sin; a.sout = c.sout; a.nclass = c.nclass; a.nchunks = c.nchunks; a.ntp = c.ntp;
   a.dymin = c.dymin; a.dxmin = c.dxmin;
@@ -958,22 +694,10 @@ static int run_x3(const float* x, const void* wpack, float osc, const float* bia
   if (gx > (long long)tiles_x * tiles_y * c.nclass) gx = (long long)tiles_x * tiles_y * c.nclass;
   if (gx < 1) gx = 1;
   dim3 grid((unsigned)gx, c.ntp / wn, batch);
-  // weights: read from L2 by every wave (default), or with FVC_X3_BLDS=1 staged per channel chunk
-  // into two LDS buffers (one copy per block) where both fit next to the A buffers. Measured on
-  // MI355X: the LDS copy is 0-5 % slower -- its ds_reads cost what the L2 reads did -- so it is
-  // kept as an option (tests check both paths give identical bits).
-  int nks_max = 0;
-  for (int cl = 0; cl < c.nclass; ++cl) nks_max = c.nks[cl] > nks_max ? c.nks[cl] : nks_max;
-  a.bq = nks_max * wn * kFrag;
-  const size_t lds_bl = lds + 2 * (size_t)a.bq * 16;
-  // (one class per launch only: the weight staging follows the current work item's class)
-  const int bl = (!kSingleAcc && c.nclass == 1 && env_int("FVC_X3_BLDS", 0) != 0 && lds_bl <= 160 * 1024) ? 1 : 0;
-  if (bl) lds = lds_bl;
-  else a.bq = 0;
   switch (c.cc) {
-    case 8: return x3_launch_cc<8>(c.wm, wn, bl, in_op, a, grid, lds, s);
-    case 16: return x3_launch_cc<16>(c.wm, wn, bl, in_op, a, grid, lds, s);
-    case 32: return x3_launch_cc<32>(c.wm, wn, bl, in_op, a, grid, lds, s);
+    case 8: return x3_launch_cc<8>(c.wm, wn, in_op, post_op, a, grid, lds, s);
+    case 16: return x3_launch_cc<16>(c.wm, wn, in_op, post_op, a, grid, lds, s);
+    case 32: return x3_launch_cc<32>(c.wm, wn, in_op, post_op, a, grid, lds, s);
   }
   return FVC_EINVAL;
 }
@@ -1023,11 +747,7 @@ int fvc_conv_x3_pack_weight(const float* w, void* wp, float* osc_out, int cin, i
                                           : w[(((size_t)j * cin + ci) * ks + ky) * ks + kx]) * sc;
               const _Float16 hi = (_Float16)v;
               out[frag + e] = hi;  // plane 0 (hi): lanes 0..63
-              if (kSingleAcc) {
-                out[frag + 64 * 8 + e] = (_Float16)(v - (float)hi);              // plane 1: lo, unscaled
-              } else {
-                out[frag + 64 * 8 + e] = (_Float16)((v - (float)hi) * 2048.f);   // plane 1: lo * 2^11
-              }
+              out[frag + 64 * 8 + e] = (_Float16)((v - (float)hi) * 2048.f);   // plane 1: lo * 2^11
             }
           }
   return 0;
