@@ -13,9 +13,16 @@ pytestmark = pytest.mark.gpu
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
 
 # fp32 tolerances (north star: recon within 1e-4 dB PSNR; symbols per SURVEY §7 tiers)
-TOL_TENSOR = 2e-4      # relative to tensor max-abs, per stage
+TOL_TENSOR = 2e-4      # relative to tensor max-abs (GOP chain / 1080p stage checks)
+# per-stage max deviation from the reference's golden tensors, relative to the tensor's max-abs
+# (measured r2 on MI355X over the three fixture sizes: estmv 5.1e-5 -- SpyNet's warp-and-refine
+# iterations amplify ulp differences --, mvfeature 7.3e-6, others <= 5.5e-6), and the clipped
+# reconstruction's absolute deviation (measured <= 8.1e-6; SURVEY §8(c) asks <= 1e-5)
+TOL_STAGE = {"estmv": 1e-4, "mvfeature": 2e-5, "mv_up": 1e-5, "warpframe": 2e-5, "prediction": 1e-5,
+             "feature": 1e-5, "z": 1e-5, "sigma": 1e-5}
+TOL_CLIPPED_ABS = 1e-5
 TOL_PSNR_DB = 1e-4
-TOL_SYMBOL_FLIP = 1e-3  # fraction of symbols allowed to differ at these tiny sizes (expect 0)
+TOL_SYMBOL_FLIP = 1e-3  # fraction of symbols allowed to differ at these tiny sizes (0 observed)
 
 
 @pytest.fixture(scope="module")
@@ -46,9 +53,11 @@ def test_forward_vs_golden(model, dev, size):
         scale = np.abs(exp).max() + 1e-6
         err = np.abs(got - exp).max()
         measured[name] = float(err / scale)
-        assert err <= TOL_TENSOR * scale, f"{name}: {err:.3e} vs {scale:.3e}"
     measured["clipped_abs"] = float(np.abs(out[0].cpu().numpy() - g["clipped"]).max())
     print(f"golden {size} max rel dev per stage:", measured)
+    for name in STAGES:
+        assert measured[name] <= TOL_STAGE[name], (name, measured)
+    assert measured["clipped_abs"] <= TOL_CLIPPED_ABS, measured
     for name, gname in (("mvfeature", "quant_mv"), ("feature", "compressed_feature"), ("z", "compressed_z")):
         got = np.round(nhwc_to_nchw(t[name], STAGES[name]).numpy())
         flips = float((got != g[gname]).mean())
@@ -58,7 +67,7 @@ def test_forward_vs_golden(model, dev, size):
         o = o.cpu().numpy()
         exp = g[n]
         if n == "clipped":
-            assert np.abs(o - exp).max() <= 5e-3
+            continue  # checked above against TOL_CLIPPED_ABS
         else:
             assert abs(float(o) - float(exp)) <= 2e-4 * abs(float(exp)) + 1e-7, (n, float(o), float(exp))
     psnr_got = 10 * np.log10(1.0 / float(out[1]))
