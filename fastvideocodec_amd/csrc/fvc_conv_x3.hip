@@ -78,6 +78,7 @@ struct X3Args {
   int ps;                          // LDS plane stride (halves): 8 x (pixels rounded to 8 mod 16)
   unsigned y_bytes;                // bytes of y (and res): < 4 GB - 4 KB, the buffer range
   unsigned x_bytes;                // bytes of one input image: < 4 GB - 4 KB
+  int ws;                          // wave-specialised launch (host dispatch only)
   int* ovf;                        // caller's overflow flag (device int; may be null)
   int toff[4][kMaxTapsX + 1];      // LDS offset (halves) of each tap's window; 0 past ntaps
 };
@@ -119,13 +120,18 @@ __device__ __forceinline__ void split8(const float (&v)[8], h8& hi, h8& lo, floa
 constexpr unsigned kOob = 0xFFFFFF00u;
 constexpr int kRsrcFlags = 0x00020000;
 
-template <int CC, int WM, int WN, int IOP, int POST>
+// WS = 0: all 8 waves (2 per SIMD) stage the next chunk's input tile between their MFMAs and
+// compute; WS = 1 (wave-specialised): waves 0-3 (one per SIMD) only compute -- their k-loop issues
+// LDS reads, L2 weight loads and MFMAs, nothing that waits on HBM -- while waves 4-7 stage the next
+// chunk (HBM loads, split, LDS writes), meeting at the per-chunk barrier.
+template <int CC, int WM, int WN, int IOP, int POST, int WS>
 __global__ __launch_bounds__(512) void conv_x3_kernel(const X3Args a) {
-  constexpr int NW = 8;
+  constexpr int NW = WS ? 4 : 8;     // compute waves
   constexpr int C8 = CC / 8;
   constexpr int TH = NW * WM;
   constexpr int TW = 32;
-  constexpr int NT = NW * 64;
+  constexpr int NT = 512;            // threads staging the first tile
+  constexpr int NTS = WS ? 256 : 512;  // threads staging later chunks
 
   extern __shared__ __attribute__((aligned(16))) _Float16 smh[];
   const int tile_h = 2 * C8 * a.ps;  // halves per A buffer: 2*C8 planes (hi octets, lo octets)
@@ -160,7 +166,8 @@ __global__ __launch_bounds__(512) void conv_x3_kernel(const X3Args a) {
   const int hf = a.half;
   const int nch = a.nchunks;
   const int tile_items = a.ir * a.ic * C8;
-  const int nstage = (tile_items + NT - 1) / NT;
+  const int nstage = (tile_items + NTS - 1) / NTS;
+  const int stid = WS ? tid - 256 : tid;  // staging thread index (loader waves under WS)
   const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(a.x + (size_t)b * a.H * a.W * a.cinp), (short)0, (int)a.x_bytes, kRsrcFlags);
   const uint4* wcls = a.w + a.wcls[cls];  // (cls, nq, wcls, tap_tab: updated per work item)
@@ -308,6 +315,34 @@ __global__ __launch_bounds__(512) void conv_x3_kernel(const X3Args a) {
         mfmas(use);
         __builtin_amdgcn_sched_barrier(0);
       };
+      if constexpr (WS) {
+        if (wave >= NW) {  // loader waves: the whole next chunk, four items in flight at a time
+          if (stage_next) {
+            for (int qs = 0; qs < nstage; qs += 4) {
+              Stage st[4];
+#pragma unroll
+              for (int u = 0; u < 4; ++u) fetch(stid + (qs + u) * NTS, s_tile, s_ch, st[u]);
+#pragma unroll
+              for (int u = 0; u < 4; ++u)
+                if (qs + u < nstage) store(nxt, st[u]);
+            }
+          }
+          __syncthreads();
+          buf ^= 1;
+          continue;
+        }
+        Ops S0, S1;
+        load(0, S0);
+        int q = 0;
+        for (; q + 1 < nq; q += 2) {
+          half_plain(q, S0, S1);
+          half_plain(q + 1, S1, S0);
+        }
+        if (nq & 1) mfmas(S0);
+        __syncthreads();
+        buf ^= 1;
+        continue;
+      }
       int staged = 0;
       Ops S0, S1;
       load(0, S0);
@@ -323,7 +358,7 @@ __global__ __launch_bounds__(512) void conv_x3_kernel(const X3Args a) {
         // loads have two half-steps of MFMAs (both waves of the SIMD) to land behind
         load(q + 1 < nq ? q + 1 : nq - 1, S1);
         Stage st;
-        fetch(tid + staged * NT, s_tile, s_ch, st);
+        fetch(stid + staged * NTS, s_tile, s_ch, st);
         __builtin_amdgcn_sched_barrier(0);
         mfmas(S0);
         __builtin_amdgcn_sched_barrier(0);
@@ -346,7 +381,7 @@ __global__ __launch_bounds__(512) void conv_x3_kernel(const X3Args a) {
       if (stage_next) {
         for (int qs = staged; qs < nstage; ++qs) {
           Stage st;
-          fetch(tid + qs * NT, s_tile, s_ch, st);
+          fetch(stid + qs * NTS, s_tile, s_ch, st);
           store(nxt, st);
         }
       }
@@ -354,6 +389,7 @@ __global__ __launch_bounds__(512) void conv_x3_kernel(const X3Args a) {
       buf ^= 1;
     }
 
+    if (WS && wave >= NW) continue;  // the loader waves have no accumulators
     // epilogue of this tile (its global stores drain while the next tile's k-loop runs).
     // Lane (li, lh) holds pixel qx0 + li of strip m; register group g (r = 4g..4g+3) holds output
     // channels N-tile*32 + 8g + 4lh + {0..3} -> one 16-B store (and residual load) per group.
@@ -559,14 +595,20 @@ static int x3_kw(const float* w, size_t n) {
   return kw < -100 ? -100 : (kw > 100 ? 100 : kw);
 }
 
-template <int CC, int WM, int WN, int IOP, int POST>
-static int x3_launch(const X3Args& a, dim3 grid, size_t lds, hipStream_t s) {
+template <int CC, int WM, int WN, int IOP, int POST, int WS>
+static int x3_launch_ws(const X3Args& a, dim3 grid, size_t lds, hipStream_t s) {
   if (lds > 64 * 1024)
-    (void)hipFuncSetAttribute((const void*)conv_x3_kernel<CC, WM, WN, IOP, POST>,
+    (void)hipFuncSetAttribute((const void*)conv_x3_kernel<CC, WM, WN, IOP, POST, WS>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL((conv_x3_kernel<CC, WM, WN, IOP, POST>), grid, dim3(512), lds, s, a);
+  hipLaunchKernelGGL((conv_x3_kernel<CC, WM, WN, IOP, POST, WS>), grid, dim3(512), lds, s, a);
   FVC_CHECK_LAUNCH();
   return 0;
+}
+
+template <int CC, int WM, int WN, int IOP, int POST>
+static int x3_launch(const X3Args& a, dim3 grid, size_t lds, hipStream_t s) {
+  if (a.ws) return x3_launch_ws<CC, WM, WN, IOP, POST, 1>(a, grid, lds, s);
+  return x3_launch_ws<CC, WM, WN, IOP, POST, 0>(a, grid, lds, s);
 }
 
 // exp after the epilogue is only ever taken with an untransformed input (Synthesis_prior_net
@@ -638,7 +680,12 @@ static int run_x3(const float* x, const void* wpack, float osc, const float* bia
   a.ovf = ovf;
   a.sin = c.sin; a.sout = c.sout; a.nclass = c.nclass; a.nchunks = c.nchunks; a.ntp = c.ntp;
   a.dymin = c.dymin; a.dxmin = c.dxmin;
-  a.ir = (c.th - 1) * c.sin + 1 + (c.dymax - c.dymin);
+  // FVC_X3_WS=1 (experiment): wave-specialised blocks, 4 compute waves -> half the tile height
+  // (same channel chunk, so the weight pack is unchanged)
+  const int ws = env_int("FVC_X3_WS", 0) ? 1 : 0;
+  const int th = ws ? c.th / 2 : c.th;
+  a.ir = (th - 1) * c.sin + 1 + (c.dymax - c.dymin);
+  a.ws = ws;
   a.ic = 31 * c.sin + 1 + (c.dxmax - c.dxmin);
   a.half = c.sin == 2 ? (a.ic + 1) / 2 : 0;
   a.inv_ic = 1.0f / (float)a.ic;
@@ -669,7 +716,7 @@ static int run_x3(const float* x, const void* wpack, float osc, const float* bia
   size_t lds = 1024 + 2 * x3_tile_bytes(a.ir, a.ic, c.cc);
   if (lds > 160 * 1024) return FVC_EINVAL;
   const int tiles_x = fvc_cdiv(a.Wq, 32);
-  const int tiles_y = fvc_cdiv(a.Hq, c.th);
+  const int tiles_y = fvc_cdiv(a.Hq, th);
   // N-tiles per block: 2 (each staged input element feeds 64 output channels) unless the layer
   // has too few spatial tiles x N-groups to give every CU of the persistent grid some work
   // stride-2 convs (one strip per wave) with 4 N-tiles take all 128 channels per block: the
