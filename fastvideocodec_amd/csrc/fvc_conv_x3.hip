@@ -79,6 +79,8 @@ struct X3Args {
   unsigned y_bytes;                // bytes of y (and res): < 4 GB - 4 KB, the buffer range
   unsigned x_bytes;                // bytes of one input image: < 4 GB - 4 KB
   int ws;                          // wave-specialised launch (host dispatch only)
+  int xcd;                         // XCD-aware mapping of blocks to tile runs
+  int prio;                        // raise wave priority around each MFMA cluster
   int* ovf;                        // caller's overflow flag (device int; may be null)
   int toff[4][kMaxTapsX + 1];      // LDS offset (halves) of each tap's window; 0 past ntaps
 };
@@ -157,8 +159,17 @@ __global__ __launch_bounds__(512) void conv_x3_kernel(const X3Args a) {
   // and every block gets the same mix of 4- / 2- / 1-tap classes); the staging pipeline runs on
   // across item boundaries
   const int nitems = ntiles * a.nclass;
-  const int w_begin = (int)(((long long)nitems * blockIdx.x) / gridDim.x);
-  const int w_end = (int)(((long long)nitems * (blockIdx.x + 1)) / gridDim.x);
+  // XCD-aware run assignment (a.xcd): consecutive block ids are dispatched round-robin to the 8
+  // XCDs, so logical run lb = (b % 8)-major gives each XCD's blocks one contiguous band of the
+  // image: neighbouring runs share halo rows (and all runs share weights) in that XCD's L2.
+  // Bijective for any grid size (q = G/8, r = G%8: the first r XCDs get q+1 runs).
+  int lb = blockIdx.x;
+  if (a.xcd) {
+    const int G = gridDim.x, q8 = G / 8, r8 = G % 8, x8 = lb % 8;
+    lb = (x8 < r8 ? x8 * (q8 + 1) : r8 * (q8 + 1) + (x8 - r8) * q8) + lb / 8;
+  }
+  const int w_begin = (int)(((long long)nitems * lb) / gridDim.x);
+  const int w_end = (int)(((long long)nitems * (lb + 1)) / gridDim.x);
   if (w_begin >= w_end) return;
   const int nt0 = blockIdx.y * WN;
   int cls = w_begin % a.nclass;
@@ -298,6 +309,7 @@ __global__ __launch_bounds__(512) void conv_x3_kernel(const X3Args a) {
       // each lane ends up with 4 consecutive channels of one pixel per register group (16-B
       // epilogue stores)
       auto mfmas = [&](const Ops& op) {
+        if (a.prio) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int m = 0; m < WM; ++m)
 #pragma unroll
@@ -308,6 +320,7 @@ __global__ __launch_bounds__(512) void conv_x3_kernel(const X3Args a) {
             cor[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wl, op.ah[m], cor[m][n], 0, 0, 0);
             cor[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wh, op.al[m], cor[m][n], 0, 0, 0);
           }
+        if (a.prio) __builtin_amdgcn_s_setprio(0);
       };
       auto half_plain = [&](int q, const Ops& use, Ops& nxt_ops) {
         load(q + 1 < nq ? q + 1 : nq - 1, nxt_ops);
@@ -686,6 +699,8 @@ static int run_x3(const float* x, const void* wpack, float osc, const float* bia
   const int th = ws ? c.th / 2 : c.th;
   a.ir = (th - 1) * c.sin + 1 + (c.dymax - c.dymin);
   a.ws = ws;
+  a.xcd = env_int("FVC_X3_XCD", 1) ? 1 : 0;
+  a.prio = env_int("FVC_X3_PRIO", 0) ? 1 : 0;
   a.ic = 31 * c.sin + 1 + (c.dxmax - c.dxmin);
   a.half = c.sin == 2 ? (a.ic + 1) / 2 : 0;
   a.inv_ic = 1.0f / (float)a.ic;
