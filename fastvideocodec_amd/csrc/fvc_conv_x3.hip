@@ -329,14 +329,14 @@ __global__ __launch_bounds__(512) void conv_x3_kernel(const X3Args a) {
         __builtin_amdgcn_sched_barrier(0);
       };
       if constexpr (WS) {
-        if (wave >= NW) {  // loader waves: the whole next chunk, four items in flight at a time
+        if (wave >= NW) {  // loader waves: the whole next chunk, two items in flight at a time
           if (stage_next) {
-            for (int qs = 0; qs < nstage; qs += 4) {
-              Stage st[4];
+            for (int qs = 0; qs < nstage; qs += 2) {
+              Stage st[2];
 #pragma unroll
-              for (int u = 0; u < 4; ++u) fetch(stid + (qs + u) * NTS, s_tile, s_ch, st[u]);
+              for (int u = 0; u < 2; ++u) fetch(stid + (qs + u) * NTS, s_tile, s_ch, st[u]);
 #pragma unroll
-              for (int u = 0; u < 4; ++u)
+              for (int u = 0; u < 2; ++u)
                 if (qs + u < nstage) store(nxt, st[u]);
             }
           }
@@ -344,14 +344,25 @@ __global__ __launch_bounds__(512) void conv_x3_kernel(const X3Args a) {
           buf ^= 1;
           continue;
         }
-        Ops S0, S1;
+        // prefetch distance 2 (three operand sets: the compute waves hold no staging registers):
+        // step q multiplies S[q % 3] while the loads of step q + 2 are in flight
+        Ops S0, S1, S2;
         load(0, S0);
+        load(nq > 1 ? 1 : 0, S1);
+        auto step = [&](int qq, const Ops& use, Ops& nxt_ops) {
+          load(qq + 2 < nq ? qq + 2 : nq - 1, nxt_ops);
+          __builtin_amdgcn_sched_barrier(0);
+          mfmas(use);
+          __builtin_amdgcn_sched_barrier(0);
+        };
         int q = 0;
-        for (; q + 1 < nq; q += 2) {
-          half_plain(q, S0, S1);
-          half_plain(q + 1, S1, S0);
+        for (; q + 2 < nq; q += 3) {
+          step(q, S0, S2);
+          step(q + 1, S1, S0);
+          step(q + 2, S2, S1);
         }
-        if (nq & 1) mfmas(S0);
+        if (q < nq) mfmas(S0);
+        if (q + 1 < nq) mfmas(S1);
         __syncthreads();
         buf ^= 1;
         continue;
