@@ -78,7 +78,6 @@ struct X3Args {
   int ps;                          // LDS plane stride (halves): 8 x (pixels rounded to 8 mod 16)
   unsigned y_bytes;                // bytes of y (and res): < 4 GB - 4 KB, the buffer range
   unsigned x_bytes;                // bytes of one input image: < 4 GB - 4 KB
-  int ws;                          // wave-specialised launch (host dispatch only)
   int xcd;                         // XCD-aware mapping of blocks to tile runs
   int prio;                        // raise wave priority around each MFMA cluster
   int* ovf;                        // caller's overflow flag (device int; may be null)
@@ -122,18 +121,19 @@ __device__ __forceinline__ void split8(const float (&v)[8], h8& hi, h8& lo, floa
 constexpr unsigned kOob = 0xFFFFFF00u;
 constexpr int kRsrcFlags = 0x00020000;
 
-// WS = 0: all 8 waves (2 per SIMD) stage the next chunk's input tile between their MFMAs and
-// compute; WS = 1 (wave-specialised): waves 0-3 (one per SIMD) only compute -- their k-loop issues
-// LDS reads, L2 weight loads and MFMAs, nothing that waits on HBM -- while waves 4-7 stage the next
-// chunk (HBM loads, split, LDS writes), meeting at the per-chunk barrier.
-template <int CC, int WM, int WN, int IOP, int POST, int WS>
+// Wave grid: the 8 waves form WG groups along N; the 8/WG waves of a group stack vertically,
+// each WM strips x WN N-tiles, and group g owns N-tiles nt0 + g*WN .. +WN-1 of the block. With
+// WG = 2, WM = 4, WN = 1 a wave re-uses each weight fragment on 4 strips: half the weight bytes
+// per MFMA of WG = 1, WM = 2, WN = 2 through the vector-memory return path (TD), which the PMC
+// passes show as the kernel's binding unit (scripts/gpu_pmc_x3.sh: TD busy 77 % at 40 % MFMA).
+template <int CC, int WM, int WN, int WG, int IOP, int POST>
 __global__ __launch_bounds__(512) void conv_x3_kernel(const X3Args a) {
-  constexpr int NW = WS ? 4 : 8;     // compute waves
+  constexpr int NW = 8 / WG;         // waves stacked vertically per N-group
   constexpr int C8 = CC / 8;
   constexpr int TH = NW * WM;
   constexpr int TW = 32;
   constexpr int NT = 512;            // threads staging the first tile
-  constexpr int NTS = WS ? 256 : 512;  // threads staging later chunks
+  constexpr int NTS = 512;           // threads staging later chunks
 
   extern __shared__ __attribute__((aligned(16))) _Float16 smh[];
   const int tile_h = 2 * C8 * a.ps;  // halves per A buffer: 2*C8 planes (hi octets, lo octets)
@@ -142,7 +142,7 @@ __global__ __launch_bounds__(512) void conv_x3_kernel(const X3Args a) {
   // LDS header (1 KB): bias of this block's N-tiles [WN * 32] floats at bytes 0..511, the staging
   // sink at 512..543
   float* const sbias = reinterpret_cast<float*>(smh);
-  static_assert(WN * 32 * 4 <= 512, "bias area");
+  static_assert(WG * WN * 32 * 4 <= 512, "bias area");
   _Float16* const sdump = smh + 256;  // 32 B sink for staging writes of items past the tile
 
   const int tid = threadIdx.x;
@@ -171,14 +171,14 @@ __global__ __launch_bounds__(512) void conv_x3_kernel(const X3Args a) {
   const int w_begin = (int)(((long long)nitems * lb) / gridDim.x);
   const int w_end = (int)(((long long)nitems * (lb + 1)) / gridDim.x);
   if (w_begin >= w_end) return;
-  const int nt0 = blockIdx.y * WN;
+  const int nt0 = blockIdx.y * (WG * WN);  // first N-tile of the block
   int cls = w_begin % a.nclass;
   int nq = a.nks[cls];
   const int hf = a.half;
   const int nch = a.nchunks;
   const int tile_items = a.ir * a.ic * C8;
   const int nstage = (tile_items + NTS - 1) / NTS;
-  const int stid = WS ? tid - 256 : tid;  // staging thread index (loader waves under WS)
+  const int stid = tid;  // staging thread index
   const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(a.x + (size_t)b * a.H * a.W * a.cinp), (short)0, (int)a.x_bytes, kRsrcFlags);
   const uint4* wcls = a.w + a.wcls[cls];  // (cls, nq, wcls, tap_tab: updated per work item)
@@ -228,12 +228,15 @@ __global__ __launch_bounds__(512) void conv_x3_kernel(const X3Args a) {
     fetch(e, w_begin / a.nclass, 0, st);
     store(tile0, st);
   }
-  if (tid < WN * 32) {
+  if (tid < WG * WN * 32) {
     const int j = nt0 * 32 + tid;
     sbias[tid] = j < a.cout ? a.bias[j] : 0.f;
   }
 
-  const int pix0 = (((wave * WM) * a.sin) * a.ic + li) * 8;  // strip m adds m * pix_m (halves)
+  const int wm_ = wave % NW;                // vertical position of this wave in its group
+  const int wg_ = wave / NW;                // N-group of this wave
+  const int ntw = nt0 + wg_ * WN;           // first N-tile of this wave
+  const int pix0 = (((wm_ * WM) * a.sin) * a.ic + li) * 8;  // strip m adds m * pix_m (halves)
   const int pix_m = a.sin * a.ic * 8;
   // tap window offsets live one per lane; v_readlane turns them into wave-uniform scalars
   // without a memory wait inside the k-loop
@@ -298,7 +301,7 @@ __global__ __launch_bounds__(512) void conv_x3_kernel(const X3Args a) {
           op.ah[m] = *reinterpret_cast<const h8*>(cur + pix0 + m * pix_m + toff);
           op.al[m] = *reinterpret_cast<const h8*>(cur + pix0 + m * pix_m + toff + C8 * a.ps);
         }
-        const uint4* wk = wch + ((size_t)q * a.ntp + nt0) * kFrag + lane;
+        const uint4* wk = wch + ((size_t)q * a.ntp + ntw) * kFrag + lane;
 #pragma unroll
         for (int n = 0; n < WN; ++n) {
           op.bh[n] = wk[n * kFrag];
@@ -328,45 +331,6 @@ __global__ __launch_bounds__(512) void conv_x3_kernel(const X3Args a) {
         mfmas(use);
         __builtin_amdgcn_sched_barrier(0);
       };
-      if constexpr (WS) {
-        if (wave >= NW) {  // loader waves: the whole next chunk, two items in flight at a time
-          if (stage_next) {
-            for (int qs = 0; qs < nstage; qs += 2) {
-              Stage st[2];
-#pragma unroll
-              for (int u = 0; u < 2; ++u) fetch(stid + (qs + u) * NTS, s_tile, s_ch, st[u]);
-#pragma unroll
-              for (int u = 0; u < 2; ++u)
-                if (qs + u < nstage) store(nxt, st[u]);
-            }
-          }
-          __syncthreads();
-          buf ^= 1;
-          continue;
-        }
-        // prefetch distance 2 (three operand sets: the compute waves hold no staging registers):
-        // step q multiplies S[q % 3] while the loads of step q + 2 are in flight
-        Ops S0, S1, S2;
-        load(0, S0);
-        load(nq > 1 ? 1 : 0, S1);
-        auto step = [&](int qq, const Ops& use, Ops& nxt_ops) {
-          load(qq + 2 < nq ? qq + 2 : nq - 1, nxt_ops);
-          __builtin_amdgcn_sched_barrier(0);
-          mfmas(use);
-          __builtin_amdgcn_sched_barrier(0);
-        };
-        int q = 0;
-        for (; q + 2 < nq; q += 3) {
-          step(q, S0, S2);
-          step(q + 1, S1, S0);
-          step(q + 2, S2, S1);
-        }
-        if (q < nq) mfmas(S0);
-        if (q + 1 < nq) mfmas(S1);
-        __syncthreads();
-        buf ^= 1;
-        continue;
-      }
       int staged = 0;
       Ops S0, S1;
       load(0, S0);
@@ -413,7 +377,6 @@ __global__ __launch_bounds__(512) void conv_x3_kernel(const X3Args a) {
       buf ^= 1;
     }
 
-    if (WS && wave >= NW) continue;  // the loader waves have no accumulators
     // epilogue of this tile (its global stores drain while the next tile's k-loop runs).
     // Lane (li, lh) holds pixel qx0 + li of strip m; register group g (r = 4g..4g+3) holds output
     // channels N-tile*32 + 8g + 4lh + {0..3} -> one 16-B store (and residual load) per group.
@@ -423,9 +386,9 @@ __global__ __launch_bounds__(512) void conv_x3_kernel(const X3Args a) {
     const int qy0 = (tile / tiles_x) * TH, qx0 = (tile % tiles_x) * TW;
     const bool px_ok = qx0 + li < a.Wq;
     auto voff_of = [&](int m, int n) {
-      const unsigned qy = qy0 + wave * WM + m;
+      const unsigned qy = qy0 + wm_ * WM + m;
       return (((unsigned)b * a.Ho + qy * a.sout + a.oy0[cls]) * a.Wo + a.ox0[cls] +
-              (unsigned)(qx0 + li) * a.sout) * (unsigned)a.coutp * 4u + (unsigned)((nt0 + n) * 32 + 4 * lh) * 4u;
+              (unsigned)(qx0 + li) * a.sout) * (unsigned)a.coutp * 4u + (unsigned)((ntw + n) * 32 + 4 * lh) * 4u;
     };
     // residual: the 4 groups of output tile t+1 are loaded before tile t is finished and stored,
     // so each wait covers loads issued one tile earlier (vmcnt is in order and counts the stores);
@@ -448,12 +411,12 @@ __global__ __launch_bounds__(512) void conv_x3_kernel(const X3Args a) {
         else if (t + 1 < NTL) load_res(t + 1, rv[(t + 1) & 1]);
       }
       const unsigned vo = voff_of(m, n);
-      const bool row_ok = qy0 + wave * WM + m < a.Hq && px_ok;
+      const bool row_ok = qy0 + wm_ * WM + m < a.Hq && px_ok;
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int jl = 8 * g + 4 * lh;       // channel within the N-tile
-        const int j0 = (nt0 + n) * 32 + jl;  // first of this lane's 4 channels
-        const float4 bj = *reinterpret_cast<const float4*>(sbias + n * 32 + jl);
+        const int j0 = (ntw + n) * 32 + jl;  // first of this lane's 4 channels
+        const float4 bj = *reinterpret_cast<const float4*>(sbias + (wg_ * WN + n) * 32 + jl);
         const float bb[4] = {bj.x, bj.y, bj.z, bj.w};
         float v[4];
 #pragma unroll
@@ -619,47 +582,42 @@ static int x3_kw(const float* w, size_t n) {
   return kw < -100 ? -100 : (kw > 100 ? 100 : kw);
 }
 
-template <int CC, int WM, int WN, int IOP, int POST, int WS>
-static int x3_launch_ws(const X3Args& a, dim3 grid, size_t lds, hipStream_t s) {
+template <int CC, int WM, int WN, int WG, int IOP, int POST>
+static int x3_launch(const X3Args& a, dim3 grid, size_t lds, hipStream_t s) {
   if (lds > 64 * 1024)
-    (void)hipFuncSetAttribute((const void*)conv_x3_kernel<CC, WM, WN, IOP, POST, WS>,
+    (void)hipFuncSetAttribute((const void*)conv_x3_kernel<CC, WM, WN, WG, IOP, POST>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL((conv_x3_kernel<CC, WM, WN, IOP, POST, WS>), grid, dim3(512), lds, s, a);
+  hipLaunchKernelGGL((conv_x3_kernel<CC, WM, WN, WG, IOP, POST>), grid, dim3(512), lds, s, a);
   FVC_CHECK_LAUNCH();
   return 0;
 }
 
-template <int CC, int WM, int WN, int IOP, int POST>
-static int x3_launch(const X3Args& a, dim3 grid, size_t lds, hipStream_t s) {
-  if (a.ws) return x3_launch_ws<CC, WM, WN, IOP, POST, 1>(a, grid, lds, s);
-  return x3_launch_ws<CC, WM, WN, IOP, POST, 0>(a, grid, lds, s);
-}
-
 // exp after the epilogue is only ever taken with an untransformed input (Synthesis_prior_net
 // deconv3, synthesis_prior.py:25,57): instantiated for IN_NONE only
-template <int CC, int WM, int WN>
+template <int CC, int WM, int WN, int WG>
 static int x3_launch_iop(int iop, int post, const X3Args& a, dim3 grid, size_t lds, hipStream_t s) {
   if (post == FVC_POST_EXP)
-    return iop == FVC_IN_NONE ? x3_launch<CC, WM, WN, FVC_IN_NONE, FVC_POST_EXP>(a, grid, lds, s) : FVC_EINVAL;
+    return iop == FVC_IN_NONE ? x3_launch<CC, WM, WN, WG, FVC_IN_NONE, FVC_POST_EXP>(a, grid, lds, s) : FVC_EINVAL;
   switch (iop) {
-    case FVC_IN_NONE: return x3_launch<CC, WM, WN, FVC_IN_NONE, FVC_POST_NONE>(a, grid, lds, s);
-    case FVC_IN_RELU: return x3_launch<CC, WM, WN, FVC_IN_RELU, FVC_POST_NONE>(a, grid, lds, s);
-    case FVC_IN_ABS: return x3_launch<CC, WM, WN, FVC_IN_ABS, FVC_POST_NONE>(a, grid, lds, s);
-    case FVC_IN_ROUND: return x3_launch<CC, WM, WN, FVC_IN_ROUND, FVC_POST_NONE>(a, grid, lds, s);
+    case FVC_IN_NONE: return x3_launch<CC, WM, WN, WG, FVC_IN_NONE, FVC_POST_NONE>(a, grid, lds, s);
+    case FVC_IN_RELU: return x3_launch<CC, WM, WN, WG, FVC_IN_RELU, FVC_POST_NONE>(a, grid, lds, s);
+    case FVC_IN_ABS: return x3_launch<CC, WM, WN, WG, FVC_IN_ABS, FVC_POST_NONE>(a, grid, lds, s);
+    case FVC_IN_ROUND: return x3_launch<CC, WM, WN, WG, FVC_IN_ROUND, FVC_POST_NONE>(a, grid, lds, s);
   }
   return FVC_EINVAL;
 }
 
-// instantiated shapes (8 waves, 2 per SIMD, <= 256 registers: scripts/kres.sh): WM, WN in {1, 2}
-// and WM = 1 with WN = 4
+// instantiated wave grids (8 waves, 2 per SIMD, <= 256 registers: scripts/kres.sh):
+// WG = 1 with WM, WN in {1, 2} or WM = 1, WN = 4; WG = 2 with WM = 4, WN = 1
 template <int CC>
-static int x3_launch_cc(int wm, int wn, int iop, int post, const X3Args& a, dim3 grid, size_t lds,
+static int x3_launch_cc(int wm, int wn, int wg, int iop, int post, const X3Args& a, dim3 grid, size_t lds,
                         hipStream_t s) {
-  if (wm == 2 && wn == 2) return x3_launch_iop<CC, 2, 2>(iop, post, a, grid, lds, s);
-  if (wm == 2 && wn == 1) return x3_launch_iop<CC, 2, 1>(iop, post, a, grid, lds, s);
-  if (wm == 1 && wn == 2) return x3_launch_iop<CC, 1, 2>(iop, post, a, grid, lds, s);
-  if (wm == 1 && wn == 1) return x3_launch_iop<CC, 1, 1>(iop, post, a, grid, lds, s);
-  if (wm == 1 && wn == 4) return x3_launch_iop<CC, 1, 4>(iop, post, a, grid, lds, s);
+  if (wg == 2) return (wm == 4 && wn == 1) ? x3_launch_iop<CC, 4, 1, 2>(iop, post, a, grid, lds, s) : FVC_EINVAL;
+  if (wm == 2 && wn == 2) return x3_launch_iop<CC, 2, 2, 1>(iop, post, a, grid, lds, s);
+  if (wm == 2 && wn == 1) return x3_launch_iop<CC, 2, 1, 1>(iop, post, a, grid, lds, s);
+  if (wm == 1 && wn == 2) return x3_launch_iop<CC, 1, 2, 1>(iop, post, a, grid, lds, s);
+  if (wm == 1 && wn == 1) return x3_launch_iop<CC, 1, 1, 1>(iop, post, a, grid, lds, s);
+  if (wm == 1 && wn == 4) return x3_launch_iop<CC, 1, 4, 1>(iop, post, a, grid, lds, s);
   return FVC_EINVAL;
 }
 
@@ -704,12 +662,8 @@ static int run_x3(const float* x, const void* wpack, float osc, const float* bia
   a.ovf = ovf;
   a.sin = c.sin; a.sout = c.sout; a.nclass = c.nclass; a.nchunks = c.nchunks; a.ntp = c.ntp;
   a.dymin = c.dymin; a.dxmin = c.dxmin;
-  // FVC_X3_WS=1 (experiment): wave-specialised blocks, 4 compute waves -> half the tile height
-  // (same channel chunk, so the weight pack is unchanged)
-  const int ws = env_int("FVC_X3_WS", 0) ? 1 : 0;
-  const int th = ws ? c.th / 2 : c.th;
+  const int th = c.th;
   a.ir = (th - 1) * c.sin + 1 + (c.dymax - c.dymin);
-  a.ws = ws;
   a.xcd = env_int("FVC_X3_XCD", 1) ? 1 : 0;
   a.prio = env_int("FVC_X3_PRIO", 0) ? 1 : 0;
   a.ic = 31 * c.sin + 1 + (c.dxmax - c.dxmin);
@@ -754,6 +708,15 @@ static int run_x3(const float* x, const void* wpack, float osc, const float* bia
   const long long base = (long long)tiles_x * tiles_y * batch * c.nclass;
   if (!want_wn)
     while (wn > 1 && base * (c.ntp / wn) < 2LL * x3_num_cus()) wn >>= 1;
+  // two N-groups of 4 waves x 4 strips instead of 8 waves x 2 strips x 2 N-tiles (same block
+  // tile: 16 rows x 32 pixels x 64 channels): each weight fragment feeds 4 strips
+  int wm = c.wm, wg = 1;
+  if (env_int("FVC_X3_WG", 0) == 2 && c.wm == 2 && wn == 2) {
+    wm = 4;
+    wn = 1;
+    wg = 2;
+  }
+  const int nb = wn * wg;  // N-tiles per block
   // persistent grid: ~one 8-wave block per CU (FVC_X3_BPC blocks per CU), each walking a
   // contiguous run of spatial tiles
   // cu_reserve CUs are left out of the persistent grid for kernels of other streams (the
@@ -761,16 +724,16 @@ static int run_x3(const float* x, const void* wpack, float osc, const float* bia
   // block has finished its whole run, doubling the launch's time (FVC_X3_RESERVE overrides)
   const int reserve = env_int("FVC_X3_RESERVE", -1) >= 0 ? env_int("FVC_X3_RESERVE", 0) : cu_reserve;
   const int ncu = x3_num_cus() - (reserve < x3_num_cus() / 2 ? reserve : x3_num_cus() / 2);
-  const long long yz = (long long)(c.ntp / wn) * batch;
+  const long long yz = (long long)(c.ntp / nb) * batch;
   const int bpc = env_int("FVC_X3_BPC", 1);
   long long gx = ((long long)ncu * bpc + yz - 1) / yz;  // blocks over all (tile, class) items
   if (gx > (long long)tiles_x * tiles_y * c.nclass) gx = (long long)tiles_x * tiles_y * c.nclass;
   if (gx < 1) gx = 1;
-  dim3 grid((unsigned)gx, c.ntp / wn, batch);
+  dim3 grid((unsigned)gx, c.ntp / nb, batch);
   switch (c.cc) {
-    case 8: return x3_launch_cc<8>(c.wm, wn, in_op, post_op, a, grid, lds, s);
-    case 16: return x3_launch_cc<16>(c.wm, wn, in_op, post_op, a, grid, lds, s);
-    case 32: return x3_launch_cc<32>(c.wm, wn, in_op, post_op, a, grid, lds, s);
+    case 8: return x3_launch_cc<8>(wm, wn, wg, in_op, post_op, a, grid, lds, s);
+    case 16: return x3_launch_cc<16>(wm, wn, wg, in_op, post_op, a, grid, lds, s);
+    case 32: return x3_launch_cc<32>(wm, wn, wg, in_op, post_op, a, grid, lds, s);
   }
   return FVC_EINVAL;
 }
