@@ -244,11 +244,19 @@ class GpuGopJob:
         self.Hp, self.Wp = self.frames.shape[-2:]
 
     def step(self):
+        if self.args.tree:
+            from fastvideocodec_amd.tree_gop import encode_decode_tree_gop
+            encode_decode_tree_gop(self.model, self.frames, overlap=not self.args.serial)
+            return
         from fastvideocodec_amd.gop import encode_decode_gop
         encode_decode_gop(self.model, self.frames, overlap=not self.args.serial, join=False)
 
     def sync(self):
         torch.cuda.synchronize()
+
+    def _tree_layers(self):
+        from fastvideocodec_amd.tree_gop import coding_layers
+        return coding_layers(self.args.gop - 1)
 
     def after_timing(self):
         """Roofline pass: one serial GOP (single stream) with HIP events around every launch on
@@ -270,8 +278,15 @@ class GpuGopJob:
     def verify(self):
         from fastvideocodec_amd.gop import encode_decode_gop
         overflow_before = getattr(self.model, "overflow_events", 0)
-        bss, decoded, sses, encs = encode_decode_gop(self.model, self.frames, check=True,
-                                                     overlap=not self.args.serial)
+        if self.args.tree:
+            from fastvideocodec_amd.tree_gop import encode_decode_tree_gop
+            bss, dd, sses, ee = encode_decode_tree_gop(self.model, self.frames, check=True,
+                                                       overlap=not self.args.serial)
+            decoded, encs = [dd[t] for t in sorted(dd)], [ee[t] for t in sorted(ee)]
+            sses = [s / len(lay) for s, lay in zip(sses, self._tree_layers())]  # per-frame mean SSE
+        else:
+            bss, decoded, sses, encs = encode_decode_gop(self.model, self.frames, check=True,
+                                                         overlap=not self.args.serial)
         torch.cuda.synchronize()
         npx = self.units * 3 * self.Hp * self.Wp
         psnrs = [float(10 * np.log10(1.0 / (float(s[0]) / npx))) for s in sses]
@@ -328,7 +343,9 @@ def run_rank(job, args, rank, world, device):
         "vs_baseline": None,
         "dtype": "f32 (convs: fp32 operands split into fp16 hi/lo, f32 accumulate)",
         "data": "synthetic (seeded GOP generator, SURVEY.md §8(d)); seeded weights + pretrained SpyNet",
-        "config": ({"workload": f"DVC P-frame encode+decode with rANS, {res_label} GOP-{args.gop}, lambda=1024 slot",
+        "config": ({"workload": f"DVC P-frame encode+decode with rANS, {res_label} GOP-{args.gop}"
+                                f"{' as an LSVC reference tree (models.py:683-728), one batch per tree layer' if args.tree else ''}"
+                                f", lambda=1024 slot",
                     "gops_per_gpu": job.units, "frames_counted": "P-frames only (I-frame pass-through)",
                     "parallelism": f"gop-shard x{world}"} if args.views <= 0 else
                    {"workload": f"{args.views}-view DVC P-frame encode+decode with rANS, {res_label} GOP-{args.gop} "
@@ -428,6 +445,10 @@ def parse_args(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true", help="same as --cpu-baseline none")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--breakdown", action="store_true", help="print per-conv-geometry timing to stderr")
+    ap.add_argument("--tree", action="store_true",
+                    help="code each GOP as the LSVC reference tree (SURVEY §8(f)#4): one batched forward per "
+                         "tree layer instead of one per frame (a different coding structure from the headline's "
+                         "sequential DVC GOP; reported separately)")
     ap.add_argument("--serial", action="store_true",
                     help="one HIP stream (no encode/code/decode overlap): per-kernel durations are unshared")
     args = ap.parse_args(argv)
