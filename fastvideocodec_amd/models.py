@@ -111,10 +111,22 @@ def PSNR(Y1_raw, Y1_com, use_list=False):
     return out
 
 
-def I_compression(Y1_raw, I_level, model_name=""):
-    """models.py:412-429 calls bpgenc/bpgdec; BPG is out of scope: lossless pass-through
-    (bpp 0, PSNR inf)."""
-    return Y1_raw, torch.zeros((), device=Y1_raw.device), torch.full((), float("inf"), device=Y1_raw.device)
+def I_compression(Y1_raw, I_level, model_name="", codec=None):
+    """models.py:412-429: code the I-frame, return (Y1_com, bpp, psnr). The reference runs
+    bpgenc/bpgdec at quality I_level (binaries absent). codec=None (default): lossless
+    pass-through (bpp 0, PSNR inf), which the golden GOP fixtures assume; codec="dwt53": the
+    build's GPU I-frame codec (fastvideocodec_amd/iframe.py) at the BPG-style step for I_level,
+    which reconstructs k/255 frames exactly when the step is 1."""
+    if codec is None:
+        return Y1_raw, torch.zeros((), device=Y1_raw.device), torch.full((), float("inf"), device=Y1_raw.device)
+    if codec != "dwt53":
+        raise ValueError(f"unknown I-frame codec {codec!r}")
+    from . import iframe as IF
+    B, _, H, W = Y1_raw.shape
+    bs, Y1_com = IF.encode(Y1_raw.float().contiguous(), IF.iframe_step(I_level))
+    bpp = torch.tensor(bs.nbytes() * 8.0 / (B * H * W), device=Y1_raw.device)
+    psnr = torch.tensor(IF.psnr(Y1_raw, Y1_com), device=Y1_raw.device)
+    return Y1_com, bpp, psnr
 
 
 def _psnr_from_mse(m):
@@ -130,7 +142,7 @@ def parallel_compression(args, model, data, compressI=False, level=0, batch_idx=
         raise NotImplementedError(model.name)
     img_loss_list, bpp_list, psnr_list = [], [], []
     aux_loss_list, aux2_loss_list = [], []
-    x_hat, bpp_i, psnr_i = I_compression(data[0:1], model.I_level)
+    x_hat, bpp_i, psnr_i = I_compression(data[0:1], model.I_level, codec=getattr(model, "iframe_codec", None))
     data[0:1] = x_hat
     if compressI and bool(torch.isfinite(psnr_i)):
         # models.py:251-253; a lossless pass-through I-frame (PSNR inf, bpp 0) is left out of

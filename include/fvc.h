@@ -217,6 +217,31 @@ int fvc_rans_decode(const uint32_t* packed, const int64_t* pack_off, const int32
                     const int32_t* cdf_sizes, const int32_t* offsets, const void* lut,
                     int32_t* symbols, int32_t* status, fvc_stream_t stream);
 
+/* ------------------------------------------------------------------ I-frame codec
+ * Replaces the reference's BPG I-frame (models.py:412-429 I_compression: bpgenc/bpgdec through
+ * os.system; the binaries are absent). Integer pipeline, encoder == decoder bit for bit:
+ * rct_fwd: x [b][3][h][w] in [0,1] -> q = clamp(rint(255 x), 0, 255) -> JPEG 2000 RCT planes
+ *          (Y, U, V) int32 [b][3][h][w]; rct_inv: the inverse, back to k/255 floats.
+ * dwt53:   `levels` levels of the reversible LeGall 5/3 lifting wavelet over `planes` planes of
+ *          h x w (rows then columns; Mallat layout), in place; tmp is scratch of the same size;
+ *          h, w multiples of 2^levels. inverse = 1 undoes it exactly.
+ * quant:   dead-zone quantisation (step q >= 1) of every coefficient outside the level-L LL
+ *          band; inverse = 1 reconstructs sign(v) (|v| q + q/2).
+ * block_index: per (plane, bs x bs block) the Laplace scale-table index of the block's mean
+ *          |coefficient| (compressai build_indexes semantics) into bidx (uint8), expanded to a
+ *          per-coefficient int32 index for the range coder; expand_index does the expansion
+ *          alone (decoder side). */
+int fvc_iframe_rct_fwd(const float* x, int32_t* coeff, int batch, int h, int w, fvc_stream_t stream);
+int fvc_iframe_rct_inv(const int32_t* coeff, float* x, int batch, int h, int w, fvc_stream_t stream);
+int fvc_iframe_dwt53(int32_t* coeff, int32_t* tmp, int planes, int h, int w, int levels, int inverse,
+                     fvc_stream_t stream);
+int fvc_iframe_quant(int32_t* coeff, int planes, int h, int w, int levels, int q, int inverse,
+                     fvc_stream_t stream);
+int fvc_iframe_block_index(const int32_t* coeff, const float* scale_table, int n_scales, uint8_t* bidx,
+                           int32_t* idx, int planes, int h, int w, int bs, fvc_stream_t stream);
+int fvc_iframe_expand_index(const uint8_t* bidx, int32_t* idx, int planes, int h, int w, int bs,
+                            fvc_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif
