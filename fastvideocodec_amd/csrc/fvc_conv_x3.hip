@@ -80,6 +80,9 @@ struct X3Args {
   unsigned x_bytes;                // bytes of one input image: < 4 GB - 4 KB
   int xcd;                         // XCD-aware mapping of blocks to tile runs
   int prio;                        // raise wave priority around each MFMA cluster
+  int dbg;                         // FVC_X3_DBG (experiments only; wrong results): bit 0 weights
+                                   // always from k-step 0 (L1-resident), bit 1 staging always
+                                   // from tile 0 / chunk 0 (cache-resident)
   int* ovf;                        // caller's overflow flag (device int; may be null)
   int toff[4][kMaxTapsX + 1];      // LDS offset (halves) of each tap's window; 0 past ntaps
 };
@@ -200,6 +203,7 @@ __global__ __launch_bounds__(512) void conv_x3_kernel(const X3Args a) {
     const int p = e / C8;
     const int r = (int)(((float)p + 0.5f) * a.inv_ic);  // exact: p < 2^14, ic <= 128
     const int c = p - r * a.ic;
+    if (a.dbg & 2) { tile = 0; ch = 0; }
     const int iy = (tile / tiles_x) * TH * a.sin + a.dymin + r;
     const int ix = (tile % tiles_x) * TW * a.sin + a.dxmin + c;
     const bool inb = (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
@@ -301,7 +305,7 @@ __global__ __launch_bounds__(512) void conv_x3_kernel(const X3Args a) {
           op.ah[m] = *reinterpret_cast<const h8*>(cur + pix0 + m * pix_m + toff);
           op.al[m] = *reinterpret_cast<const h8*>(cur + pix0 + m * pix_m + toff + C8 * a.ps);
         }
-        const uint4* wk = wch + ((size_t)q * a.ntp + ntw) * kFrag + lane;
+        const uint4* wk = ((a.dbg & 1) ? wcls : wch) + ((size_t)((a.dbg & 1) ? 0 : q) * a.ntp + ntw) * kFrag + lane;
 #pragma unroll
         for (int n = 0; n < WN; ++n) {
           op.bh[n] = wk[n * kFrag];
@@ -666,6 +670,7 @@ static int run_x3(const float* x, const void* wpack, float osc, const float* bia
   a.ir = (th - 1) * c.sin + 1 + (c.dymax - c.dymin);
   a.xcd = env_int("FVC_X3_XCD", 1) ? 1 : 0;
   a.prio = env_int("FVC_X3_PRIO", 0) ? 1 : 0;
+  a.dbg = env_int("FVC_X3_DBG", 0);
   a.ic = 31 * c.sin + 1 + (c.dxmax - c.dxmin);
   a.half = c.sin == 2 ? (a.ic + 1) / 2 : 0;
   a.inv_ic = 1.0f / (float)a.ic;
