@@ -52,7 +52,15 @@ constexpr int kMaxTapsX = 49;
 // rejected, r2: one accumulator with UNSCALED residual halves -- 64 fewer VGPRs, same speed on
 // every geometry (scripts/gpu_x3_variants.sh), but an activation residual below 2^-14 is an
 // fp16 subnormal and small-activation layers lose accuracy: 4.8e-4 relative at |x| ~ 1e-4.)
-constexpr float kLoScale = 2048.f;  // activation residual scale
+constexpr float kLoScale = 2048.f;
+// FVC_X3_KO (compile-time, experiment builds only -- wrong results): knock out parts of the k-loop to
+// find the binding unit. bit 0: no weight loads (registers), bit 1: no staging of later chunks,
+// bit 2: no LDS operand reads (registers), bit 3: no MFMAs, bit 4: weights always from k-step 0
+// (L1-resident), bit 5: staging always from tile 0 / chunk 0 (cache-resident).
+#ifndef FVC_X3_KO
+#define FVC_X3_KO 0
+#endif
+constexpr int kKO = FVC_X3_KO;  // activation residual scale
 constexpr int kNPL = 2;                    // weight planes per (k-step, N-tile): hi, lo
 constexpr int kFrag = 64 * kNPL;          // uint4 per (k-step, N-tile)
 
@@ -79,10 +87,7 @@ struct X3Args {
   unsigned y_bytes;                // bytes of y (and res): < 4 GB - 4 KB, the buffer range
   unsigned x_bytes;                // bytes of one input image: < 4 GB - 4 KB
   int xcd;                         // XCD-aware mapping of blocks to tile runs
-  int prio;                        // raise wave priority around each MFMA cluster
-  int dbg;                         // FVC_X3_DBG (experiments only; wrong results): bit 0 weights
-                                   // always from k-step 0 (L1-resident), bit 1 staging always
-                                   // from tile 0 / chunk 0 (cache-resident)
+  int prio;                        // static priority 1 for the second-dispatched half (waves 4-7)
   int* ovf;                        // caller's overflow flag (device int; may be null)
   int toff[4][kMaxTapsX + 1];      // LDS offset (halves) of each tap's window; 0 past ntaps
 };
@@ -129,14 +134,14 @@ constexpr int kRsrcFlags = 0x00020000;
 // WG = 2, WM = 4, WN = 1 a wave re-uses each weight fragment on 4 strips: half the weight bytes
 // per MFMA of WG = 1, WM = 2, WN = 2 through the vector-memory return path (TD), which the PMC
 // passes show as the kernel's binding unit (scripts/gpu_pmc_x3.sh: TD busy 77 % at 40 % MFMA).
-template <int CC, int WM, int WN, int WG, int IOP, int POST>
-__global__ __launch_bounds__(512) void conv_x3_kernel(const X3Args a) {
-  constexpr int NW = 8 / WG;         // waves stacked vertically per N-group
+template <int CC, int WM, int WN, int WG, int IOP, int POST, int NWV>
+__global__ __launch_bounds__(NWV * 64) void conv_x3_kernel(const X3Args a) {
+  constexpr int NW = NWV / WG;       // waves stacked vertically per N-group
   constexpr int C8 = CC / 8;
   constexpr int TH = NW * WM;
   constexpr int TW = 32;
-  constexpr int NT = 512;            // threads staging the first tile
-  constexpr int NTS = 512;           // threads staging later chunks
+  constexpr int NT = NWV * 64;       // threads staging the first tile
+  constexpr int NTS = NWV * 64;      // threads staging later chunks
 
   extern __shared__ __attribute__((aligned(16))) _Float16 smh[];
   const int tile_h = 2 * C8 * a.ps;  // halves per A buffer: 2*C8 planes (hi octets, lo octets)
@@ -197,13 +202,14 @@ __global__ __launch_bounds__(512) void conv_x3_kernel(const X3Args a) {
     bool ok;
   };
   auto fetch = [&](int e, int tile, int ch, Stage& st) {
+    if constexpr ((kKO & 2) != 0) return;
     st.ok = e < tile_items;  // past the end: loads of a clamped index, no LDS write
     e = st.ok ? e : tile_items - 1;
     const int o = e & (C8 - 1);
     const int p = e / C8;
     const int r = (int)(((float)p + 0.5f) * a.inv_ic);  // exact: p < 2^14, ic <= 128
     const int c = p - r * a.ic;
-    if (a.dbg & 2) { tile = 0; ch = 0; }
+    if constexpr ((kKO & 32) != 0) { tile = 0; ch = 0; }
     const int iy = (tile / tiles_x) * TH * a.sin + a.dymin + r;
     const int ix = (tile % tiles_x) * TW * a.sin + a.dxmin + c;
     const bool inb = (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
@@ -214,6 +220,7 @@ __global__ __launch_bounds__(512) void conv_x3_kernel(const X3Args a) {
     st.dst = o * a.ps + (r * a.ic + cpos) * 8;  // plane o (hi), pixel-minor
   };
   auto store = [&](_Float16* t, const Stage& st) {
+    if constexpr ((kKO & 2) != 0) return;
     float v[8] = {st.v0.x, st.v0.y, st.v0.z, st.v0.w, st.v1.x, st.v1.y, st.v1.z, st.v1.w};
 #pragma unroll
     for (int i = 0; i < 8; ++i) v[i] = in_op_t<IOP>(v[i]);  // zero padding stays zero
@@ -237,6 +244,7 @@ __global__ __launch_bounds__(512) void conv_x3_kernel(const X3Args a) {
     sbias[tid] = j < a.cout ? a.bias[j] : 0.f;
   }
 
+  if (a.prio && wave >= NWV / 2) __builtin_amdgcn_s_setprio(1);
   const int wm_ = wave % NW;                // vertical position of this wave in its group
   const int wg_ = wave / NW;                // N-group of this wave
   const int ntw = nt0 + wg_ * WN;           // first N-tile of this wave
@@ -252,6 +260,8 @@ __global__ __launch_bounds__(512) void conv_x3_kernel(const X3Args a) {
     uint4 bh[WN], bl[WN];
   };
   f32x16 acc[WM][WN], cor[WM][WN];
+  uint4 ko_w = a.w[lane];
+  h8 ko_a = *reinterpret_cast<const h8*>(tile0 + 8 * lane);
   int buf = 0;  // LDS buffer holding the chunk being multiplied
   const __amdgpu_buffer_rsrc_t ry =
       __builtin_amdgcn_make_buffer_rsrc((void*)a.y, (short)0, (int)a.y_bytes, kRsrcFlags);
@@ -302,12 +312,22 @@ __global__ __launch_bounds__(512) void conv_x3_kernel(const X3Args a) {
         }
 #pragma unroll
         for (int m = 0; m < WM; ++m) {
+          if constexpr ((kKO & 4) != 0) {
+            op.ah[m] = ko_a + (_Float16)(q + m);
+            op.al[m] = ko_a;
+            continue;
+          }
           op.ah[m] = *reinterpret_cast<const h8*>(cur + pix0 + m * pix_m + toff);
           op.al[m] = *reinterpret_cast<const h8*>(cur + pix0 + m * pix_m + toff + C8 * a.ps);
         }
-        const uint4* wk = ((a.dbg & 1) ? wcls : wch) + ((size_t)((a.dbg & 1) ? 0 : q) * a.ntp + ntw) * kFrag + lane;
+        const uint4* wk = ((kKO & 16) ? wcls : wch) + ((size_t)((kKO & 16) ? 0 : q) * a.ntp + ntw) * kFrag + lane;
 #pragma unroll
         for (int n = 0; n < WN; ++n) {
+          if constexpr ((kKO & 1) != 0) {
+            op.bh[n] = ko_w + (unsigned)(q + n);
+            op.bl[n] = ko_w;
+            continue;
+          }
           op.bh[n] = wk[n * kFrag];
           op.bl[n] = wk[n * kFrag + 64];
         }
@@ -316,7 +336,13 @@ __global__ __launch_bounds__(512) void conv_x3_kernel(const X3Args a) {
       // each lane ends up with 4 consecutive channels of one pixel per register group (16-B
       // epilogue stores)
       auto mfmas = [&](const Ops& op) {
-        if (a.prio) __builtin_amdgcn_s_setprio(1);
+        if constexpr ((kKO & 8) != 0) {
+#pragma unroll
+          for (int m = 0; m < WM; ++m)
+#pragma unroll
+            for (int n = 0; n < WN; ++n) acc[m][n][0] += (float)op.ah[m][0] + (float)__builtin_bit_cast(h8, op.bh[n])[0];
+          return;
+        }
 #pragma unroll
         for (int m = 0; m < WM; ++m)
 #pragma unroll
@@ -327,7 +353,6 @@ __global__ __launch_bounds__(512) void conv_x3_kernel(const X3Args a) {
             cor[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wl, op.ah[m], cor[m][n], 0, 0, 0);
             cor[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wh, op.al[m], cor[m][n], 0, 0, 0);
           }
-        if (a.prio) __builtin_amdgcn_s_setprio(0);
       };
       auto half_plain = [&](int q, const Ops& use, Ops& nxt_ops) {
         load(q + 1 < nq ? q + 1 : nq - 1, nxt_ops);
@@ -586,27 +611,27 @@ static int x3_kw(const float* w, size_t n) {
   return kw < -100 ? -100 : (kw > 100 ? 100 : kw);
 }
 
-template <int CC, int WM, int WN, int WG, int IOP, int POST>
+template <int CC, int WM, int WN, int WG, int IOP, int POST, int NWV>
 static int x3_launch(const X3Args& a, dim3 grid, size_t lds, hipStream_t s) {
   if (lds > 64 * 1024)
-    (void)hipFuncSetAttribute((const void*)conv_x3_kernel<CC, WM, WN, WG, IOP, POST>,
+    (void)hipFuncSetAttribute((const void*)conv_x3_kernel<CC, WM, WN, WG, IOP, POST, NWV>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL((conv_x3_kernel<CC, WM, WN, WG, IOP, POST>), grid, dim3(512), lds, s, a);
+  hipLaunchKernelGGL((conv_x3_kernel<CC, WM, WN, WG, IOP, POST, NWV>), grid, dim3(NWV * 64), lds, s, a);
   FVC_CHECK_LAUNCH();
   return 0;
 }
 
 // exp after the epilogue is only ever taken with an untransformed input (Synthesis_prior_net
 // deconv3, synthesis_prior.py:25,57): instantiated for IN_NONE only
-template <int CC, int WM, int WN, int WG>
+template <int CC, int WM, int WN, int WG, int NWV = 8>
 static int x3_launch_iop(int iop, int post, const X3Args& a, dim3 grid, size_t lds, hipStream_t s) {
   if (post == FVC_POST_EXP)
-    return iop == FVC_IN_NONE ? x3_launch<CC, WM, WN, WG, FVC_IN_NONE, FVC_POST_EXP>(a, grid, lds, s) : FVC_EINVAL;
+    return iop == FVC_IN_NONE ? x3_launch<CC, WM, WN, WG, FVC_IN_NONE, FVC_POST_EXP, NWV>(a, grid, lds, s) : FVC_EINVAL;
   switch (iop) {
-    case FVC_IN_NONE: return x3_launch<CC, WM, WN, WG, FVC_IN_NONE, FVC_POST_NONE>(a, grid, lds, s);
-    case FVC_IN_RELU: return x3_launch<CC, WM, WN, WG, FVC_IN_RELU, FVC_POST_NONE>(a, grid, lds, s);
-    case FVC_IN_ABS: return x3_launch<CC, WM, WN, WG, FVC_IN_ABS, FVC_POST_NONE>(a, grid, lds, s);
-    case FVC_IN_ROUND: return x3_launch<CC, WM, WN, WG, FVC_IN_ROUND, FVC_POST_NONE>(a, grid, lds, s);
+    case FVC_IN_NONE: return x3_launch<CC, WM, WN, WG, FVC_IN_NONE, FVC_POST_NONE, NWV>(a, grid, lds, s);
+    case FVC_IN_RELU: return x3_launch<CC, WM, WN, WG, FVC_IN_RELU, FVC_POST_NONE, NWV>(a, grid, lds, s);
+    case FVC_IN_ABS: return x3_launch<CC, WM, WN, WG, FVC_IN_ABS, FVC_POST_NONE, NWV>(a, grid, lds, s);
+    case FVC_IN_ROUND: return x3_launch<CC, WM, WN, WG, FVC_IN_ROUND, FVC_POST_NONE, NWV>(a, grid, lds, s);
   }
   return FVC_EINVAL;
 }
@@ -614,8 +639,9 @@ static int x3_launch_iop(int iop, int post, const X3Args& a, dim3 grid, size_t l
 // instantiated wave grids (8 waves, 2 per SIMD, <= 256 registers: scripts/kres.sh):
 // WG = 1 with WM, WN in {1, 2} or WM = 1, WN = 4; WG = 2 with WM = 4, WN = 1
 template <int CC>
-static int x3_launch_cc(int wm, int wn, int wg, int iop, int post, const X3Args& a, dim3 grid, size_t lds,
-                        hipStream_t s) {
+static int x3_launch_cc(int nwv, int wm, int wn, int wg, int iop, int post, const X3Args& a, dim3 grid,
+                        size_t lds, hipStream_t s) {
+  if (nwv != 8) return FVC_EINVAL;
   if (wg == 2) return (wm == 4 && wn == 1) ? x3_launch_iop<CC, 4, 1, 2>(iop, post, a, grid, lds, s) : FVC_EINVAL;
   if (wm == 2 && wn == 2) return x3_launch_iop<CC, 2, 2, 1>(iop, post, a, grid, lds, s);
   if (wm == 2 && wn == 1) return x3_launch_iop<CC, 2, 1, 1>(iop, post, a, grid, lds, s);
@@ -670,7 +696,6 @@ static int run_x3(const float* x, const void* wpack, float osc, const float* bia
   a.ir = (th - 1) * c.sin + 1 + (c.dymax - c.dymin);
   a.xcd = env_int("FVC_X3_XCD", 1) ? 1 : 0;
   a.prio = env_int("FVC_X3_PRIO", 0) ? 1 : 0;
-  a.dbg = env_int("FVC_X3_DBG", 0);
   a.ic = 31 * c.sin + 1 + (c.dxmax - c.dxmin);
   a.half = c.sin == 2 ? (a.ic + 1) / 2 : 0;
   a.inv_ic = 1.0f / (float)a.ic;
@@ -716,7 +741,7 @@ static int run_x3(const float* x, const void* wpack, float osc, const float* bia
   // two N-groups of 4 waves x 4 strips instead of 8 waves x 2 strips x 2 N-tiles (same block
   // tile: 16 rows x 32 pixels x 64 channels): each weight fragment feeds 4 strips
   int wm = c.wm, wg = 1;
-  if (env_int("FVC_X3_WG", 0) == 2 && c.wm == 2 && wn == 2) {
+  if (c.nw == 8 && env_int("FVC_X3_WG", 0) == 2 && c.wm == 2 && wn == 2) {
     wm = 4;
     wn = 1;
     wg = 2;
@@ -736,9 +761,9 @@ static int run_x3(const float* x, const void* wpack, float osc, const float* bia
   if (gx < 1) gx = 1;
   dim3 grid((unsigned)gx, c.ntp / nb, batch);
   switch (c.cc) {
-    case 8: return x3_launch_cc<8>(wm, wn, wg, in_op, post_op, a, grid, lds, s);
-    case 16: return x3_launch_cc<16>(wm, wn, wg, in_op, post_op, a, grid, lds, s);
-    case 32: return x3_launch_cc<32>(wm, wn, wg, in_op, post_op, a, grid, lds, s);
+    case 8: return x3_launch_cc<8>(c.nw, wm, wn, wg, in_op, post_op, a, grid, lds, s);
+    case 16: return x3_launch_cc<16>(c.nw, wm, wn, wg, in_op, post_op, a, grid, lds, s);
+    case 32: return x3_launch_cc<32>(c.nw, wm, wn, wg, in_op, post_op, a, grid, lds, s);
   }
   return FVC_EINVAL;
 }
