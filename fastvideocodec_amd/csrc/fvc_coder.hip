@@ -271,109 +271,293 @@ __global__ void k_pack_copy(const uint32_t* __restrict__ words, const int64_t* _
 }
 
 
-// Decode tables, small enough to stay L2-resident: per table t
-//   lut[t][u]  (u = cum >> kLutShift, 4096 buckets): the symbol s with cdf[s] <= u << kLutShift
-//              < cdf[s+1], i.e. the first candidate for any cum in that bucket;
-//   sf[t][s]   = cdf[s] | (cdf[s+1] - cdf[s]) << 16.
-// A decoded symbol costs two dependent L2 hits (bucket, then its start/freq) plus a short
-// forward step when the bucket straddles a symbol boundary; the old 2^16-entry LUT was one
-// random access into 256 KB per table, missing in L2 almost every time.
-constexpr int kLutShift = 4;
-constexpr int kLutN = 1 << (kPrec - kLutShift);
+// Decode tables: a compact image per table, copied into the decoder's LDS table cache
+// (k_rans_decode) or read from L2 when it does not fit. Table t occupies
+// img_off[t] .. img_off[t+1] words = kL2N bucket entries of 2 words, then n_t = cdf_sizes[t] - 1
+// start|freq<<16 words (padded to an even count). Bucket u covers cum in [u << kL2Shift, (u+1) << kL2Shift): its entry is
+// {lo | hi << 16, start|freq<<16 of lo} with lo / hi the symbols holding the bucket's first / last
+// cum; lo == hi (most of the cum space) decodes from the entry alone.
+constexpr int kL2Shift = 9;
+constexpr int kL2N = 1 << (kPrec - kL2Shift);
+constexpr int kL2Words = 2 * kL2N;
 
-__global__ void k_build_lut(const int32_t* __restrict__ cdfs, int cdf_stride, const int32_t* __restrict__ cdf_sizes,
-                            int ntables, uint16_t* __restrict__ lut, uint32_t* __restrict__ sf) {
-  const int64_t nl = (int64_t)ntables * kLutN;
-  const int64_t ns = (int64_t)ntables * cdf_stride;
-  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < nl + ns; e += (int64_t)gridDim.x * blockDim.x) {
-    if (e < nl) {
-      const int t = (int)(e / kLutN);
-      const uint32_t cum = (uint32_t)(e % kLutN) << kLutShift;
-      const int32_t* cdf = cdfs + (size_t)t * cdf_stride;
-      int lo = 0, hi = cdf_sizes[t] - 1;
-      while (hi - lo > 1) {
-        const int mid = (lo + hi) >> 1;
-        if ((uint32_t)cdf[mid] <= cum) lo = mid; else hi = mid;
-      }
-      lut[e] = (uint16_t)lo;
+__global__ void k_build_img_off(const int32_t* __restrict__ cdf_sizes, int ntables, uint32_t* __restrict__ img_off) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  uint32_t o = 0;
+  for (int t = 0; t < ntables; ++t) {
+    img_off[t] = o;
+    o += kL2Words + (uint32_t)((cdf_sizes[t] - 1 + 1) & ~1);  // even: 8-B aligned bucket entries
+  }
+  img_off[ntables] = o;
+}
+
+__global__ void k_build_img(const int32_t* __restrict__ cdfs, int cdf_stride, const int32_t* __restrict__ cdf_sizes,
+                            int ntables, const uint32_t* __restrict__ img_off, uint32_t* __restrict__ img) {
+  const int t = blockIdx.y;
+  const int n = cdf_sizes[t] - 1;
+  const int32_t* cdf = cdfs + (size_t)t * cdf_stride;
+  auto sft = [&](int s) { return (uint32_t)cdf[s] | ((uint32_t)(cdf[s + 1] - cdf[s]) << 16); };
+  uint32_t* out = img + img_off[t];
+  auto holder = [&](uint32_t cum) {  // last symbol with cdf[s] <= cum
+    int lo = 0, hi = n - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if ((uint32_t)cdf[mid] <= cum) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+  };
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < kL2N + n; e += gridDim.x * blockDim.x) {
+    if (e < kL2N) {
+      const int lo = holder((uint32_t)e << kL2Shift);
+      const int hi = holder((((uint32_t)e + 1) << kL2Shift) - 1);
+      out[2 * e] = (uint32_t)lo | ((uint32_t)hi << 16);
+      out[2 * e + 1] = sft(lo);
     } else {
-      const int64_t f = e - nl;
-      const int t = (int)(f / cdf_stride);
-      const int sidx = (int)(f % cdf_stride);
-      const int32_t* cdf = cdfs + (size_t)t * cdf_stride;
-      sf[f] = sidx < cdf_sizes[t] - 1 ? ((uint32_t)cdf[sidx] | ((uint32_t)(cdf[sidx + 1] - cdf[sidx]) << 16)) : 0u;
+      out[kL2Words + e - kL2N] = sft(e - kL2N);
     }
   }
 }
 
-// One lane per stream (64-lane blocks). The next bitstream word and the next kPf table indexes
-// are held in registers ahead of need, so the only memory accesses on the state chain are the
-// two table hits. Decoded symbols go to an LDS ring (kRing per lane) and are written to global
-// memory in bursts: a global store outstanding in vmcnt would make every later load wait for it
-// (the compiler cannot order a load behind a store), i.e. one store latency per symbol.
-constexpr int kRing = 64;
+// One block per 64 streams, two waves (r2). Wave 0 (the decoder) runs the state chains, one lane per stream; wave 1
+// (the loader) keeps the decoder's inputs in LDS one phase (kJ symbols) ahead -- per symbol a
+// record {table index, offset, LDS address of the table's image or ~0} and a ring of the
+// stream's next kR bitstream words -- and writes the previous phase's decoded symbols out. The
+// decoder reads only LDS for a symbol of a cached table: its chain is one bucket-entry read
+// (plus a binary search in the rare buckets that span several symbols), the rANS arithmetic
+// and, on renormalisation, one ring read -- no L2 latency, no in-order vmcnt wait behind an HBM
+// index fetch or a store (r1's one-wave kernel had both: 4.5 -> 3.7-4.2 ms for 1,152 streams of
+// 8,160 low-rate symbols, scripts/coder_micro.py).
+//
+// Table cache: the block copies the contiguous run of table images [t_lo, t_hi) into LDS (t_lo
+// = the smallest table index among its streams' first kJ symbols; as many tables as fit in
+// kTabWords). Channel framing puts one table per stream (mv, z: a block's 64 channels) or the
+// Laplace scale table, smallest scales first (feature), in the cache; a symbol of another table
+// reads the same image from L2 (its global offset travels in the record).
+//
+// The loader hides its own latencies: table indexes are fetched two phases ahead (registers),
+// offsets of cached tables come from LDS, and the ring is refilled kRB words at a time.
+//
+// Ring protocol: the decoder publishes its word position pos(B_p) at barrier B_p and the loader
+// its fill mark (double-buffered by phase parity); during phase p the loader may write words [fill, fill + kRB) into slots w % kR
+// if fill + kRB <= pos(B_p) + kR (those slots held consumed words). During phase p the decoder
+// reads ring words below the fill mark published at B_p; a word past it is read from global.
+constexpr int kJ = 16;                // symbols per phase
+constexpr int kR = 64;                // ring words per stream
+constexpr int kRB = 32;               // ring refill batch
+constexpr int kTabDir = 256;          // cached tables at most
+constexpr int kTabWords = 25600;      // 100 KB of table images
+constexpr size_t kDec2Lds =
+    (size_t)(2 * kJ * 64 * 4 + 2 * kJ * 64 + kR * 64 + 3 * 64 + 4 + 2 * kTabDir + kTabWords) * 4;
+constexpr uint32_t kGlobTab = 0x80000000u;  // record flag: table image read from global memory
+constexpr int kRsrcFlags = 0x00020000;  // buffer descriptor dword 3 (raw 32-bit, as fvc_conv_x3.hip)
 
-__global__ __launch_bounds__(64) void k_rans_decode(
+// Global reads that sit next to LDS reads of the same value go through buffer descriptors: a
+// plain pointer would let the compiler merge the two into one generic (flat) load, which waits on
+// both counters and serialises the chain.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t dec_rsrc(const void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, -1, kRsrcFlags);
+}
+__device__ __forceinline__ uint32_t bload(__amdgpu_buffer_rsrc_t r, uint32_t byte_off) {
+  return __builtin_amdgcn_raw_buffer_load_b32(r, byte_off, 0, 0);
+}
+
+__global__ __launch_bounds__(128) void k_rans_decode(
     const uint32_t* __restrict__ packed, const int64_t* __restrict__ pack_off, const int32_t* __restrict__ indexes,
-    const int64_t* __restrict__ sym_off, int nstreams, int cdf_stride, const int32_t* __restrict__ cdf_sizes,
-    const int32_t* __restrict__ offsets, const uint16_t* __restrict__ lut, const uint32_t* __restrict__ sft,
+    const int64_t* __restrict__ sym_off, int nstreams, const int32_t* __restrict__ cdf_sizes,
+    const int32_t* __restrict__ offsets, int ntables, const uint32_t* __restrict__ img_off, const uint32_t* __restrict__ img,
     int32_t* __restrict__ symbols, int32_t* __restrict__ status) {
-  __shared__ int32_t ring[kRing * 64];
-  const int lane = threadIdx.x;
+  extern __shared__ int32_t lds[];
+  uint4* const s_rec = reinterpret_cast<uint4*>(lds);          // [2][kJ][64] {ci, off, tab, -}
+  int32_t* const s_out = lds + 2 * kJ * 64 * 4;                // [2][kJ][64] decoded symbols
+  uint32_t* const s_ring = (uint32_t*)(s_out + 2 * kJ * 64);   // [kR][64]
+  int32_t* const s_pos = (int32_t*)(s_ring + kR * 64);         // [64] published word positions
+  int32_t* const s_fill = s_pos + 64;                          // [2][64] ring fill marks by phase parity
+  int32_t* const s_trange = s_fill + 2 * 64;                   // t_lo, t_hi
+  uint32_t* const s_dir = (uint32_t*)(s_trange + 4);           // [kTabDir] LDS word offset of cached table
+  int32_t* const s_doff = (int32_t*)(s_dir + kTabDir);         // [kTabDir] its offset
+  uint32_t* const s_tab = (uint32_t*)(s_doff + kTabDir);       // [kTabWords] table images
+  const int lane = threadIdx.x & 63;
+  const bool loader = threadIdx.x >= 64;
   const int s = blockIdx.x * 64 + lane;
   const bool live = s < nstreams;
-  const uint32_t* ptr = packed + (live ? pack_off[s] : 0);
-  const uint32_t* end = packed + (live ? pack_off[s + 1] : 0);
-  bool ok = live && end - ptr >= 2;
-  uint64_t x = 0;
-  if (ok) {
-    x = (uint64_t)ptr[0] | ((uint64_t)ptr[1] << 32);
-    ptr += 2;
+  const int64_t w0 = live ? pack_off[s] : 0;
+  const int nw = live ? (int)(pack_off[s + 1] - w0) : 0;
+  const int64_t b = live ? sym_off[s] : 0;
+  const int len = live ? (int)(sym_off[s + 1] - b) : 0;
+  int maxlen = len;
+  for (int o = 32; o > 0; o >>= 1) maxlen = max(maxlen, __shfl_xor(maxlen, o, 64));
+  const int nph = (maxlen + kJ - 1) / kJ;
+  const __amdgpu_buffer_rsrc_t r_packed = dec_rsrc(packed), r_offsets = dec_rsrc(offsets);
+  const __amdgpu_buffer_rsrc_t r_img = dec_rsrc(img), r_imgoff = dec_rsrc(img_off);
+
+  // ---- loader helpers
+  int32_t ci[kJ], cn[kJ];  // table indexes of the next phase and the one after
+  auto load_ci = [&](int32_t (&dst)[kJ], int base) {
+#pragma unroll
+    for (int j = 0; j < kJ; ++j) dst[j] = base + j < len ? indexes[b + base + j] : 0;
+  };
+  auto put_recs = [&](int buf, int t_lo, int t_hi) {
+#pragma unroll
+    for (int j = 0; j < kJ; ++j) {
+      const int c = ci[j];
+      const bool cached = (unsigned)(c - t_lo) < (unsigned)(t_hi - t_lo);
+      const int di = cached ? c - t_lo : 0;  // separate LDS and global loads (no generic pointer)
+      uint32_t tab = s_dir[di];
+      int32_t off = s_doff[di];
+      if (!cached) {  // the table's image in global memory (L2-resident)
+        tab = kGlobTab | bload(r_imgoff, (uint32_t)c * 4u);
+        off = (int32_t)bload(r_offsets, (uint32_t)c * 4u);
+      }
+      s_rec[(buf * kJ + j) * 64 + lane] = make_uint4((uint32_t)c, (uint32_t)off, tab, 0u);
+    }
+  };
+  auto flush = [&](int buf, int base) {
+    int32_t v[kJ];
+#pragma unroll
+    for (int j = 0; j < kJ; ++j) v[j] = s_out[(buf * kJ + j) * 64 + lane];
+#pragma unroll
+    for (int j = 0; j < kJ; ++j)
+      if (base + j < len) symbols[b + base + j] = v[j];
+  };
+  int fill_end = 0;
+  auto refill = [&](int pub) {  // one batch of kRB words if their slots are free
+    if (fill_end >= nw || fill_end + kRB > pub + kR) return;
+    uint32_t v[kRB];
+#pragma unroll
+    for (int k = 0; k < kRB; ++k) v[k] = fill_end + k < nw ? packed[w0 + fill_end + k] : 0u;
+#pragma unroll
+    for (int k = 0; k < kRB; ++k) s_ring[((unsigned)(fill_end + k) & (kR - 1)) * 64 + lane] = v[k];
+    fill_end = min(fill_end + kRB, nw);
+  };
+
+  // ---- prologue: cache range, table images, phase-0 records, first ring words
+  if (loader) {
+    load_ci(ci, 0);
+    int tmin = ntables;
+#pragma unroll
+    for (int j = 0; j < kJ; ++j)
+      if (j < len) tmin = min(tmin, ci[j]);
+    for (int o = 32; o > 0; o >>= 1) tmin = min(tmin, __shfl_xor(tmin, o, 64));
+    int nfit = 0;  // tables tmin .. tmin + nfit - 1 fit (the test is monotone in t)
+    if (tmin < ntables) {
+      const uint32_t base = img_off[tmin];
+      for (int k0 = 0; k0 < kTabDir; k0 += 64) {
+        const int t = tmin + k0 + lane;
+        nfit += __popcll(__ballot(t < ntables && img_off[t + 1] - base <= (uint32_t)kTabWords));
+      }
+    }
+    if (lane == 0) {
+      s_trange[0] = tmin;
+      s_trange[1] = tmin + nfit;
+    }
+  } else {
+    s_pos[lane] = 0;
   }
-  uint32_t wnext = ptr < end ? *ptr : 0u;  // next renormalisation word, loaded ahead
+  __syncthreads();
+  const int t_lo = s_trange[0], t_hi = s_trange[1];
+  if (t_hi > t_lo) {
+    const uint32_t base = img_off[t_lo];
+    const uint32_t nwd = img_off[t_hi] - base;
+    for (uint32_t i = threadIdx.x; i < nwd; i += 128) s_tab[i] = img[base + i];
+    for (int t = threadIdx.x; t < t_hi - t_lo; t += 128) {
+      s_dir[t] = (uint32_t)(s_tab - (uint32_t*)lds) + img_off[t_lo + t] - base;
+      s_doff[t] = offsets[t_lo + t];
+    }
+  }
+  __syncthreads();
+  if (loader) {
+    put_recs(0, t_lo, t_hi);
+    if (nph > 1) load_ci(cn, kJ);
+    refill(0);
+    refill(0);
+    s_fill[lane] = fill_end;  // parity 0: read after B_0
+  }
+  __syncthreads();  // B_0
+
+  if (loader) {
+    for (int p = 0; p < nph; ++p) {
+      const int pub = s_pos[lane];  // pos(B_p)
+      if (p + 1 < nph) {
+#pragma unroll
+        for (int j = 0; j < kJ; ++j) ci[j] = cn[j];
+        if (p + 2 < nph) load_ci(cn, (p + 2) * kJ);
+        put_recs((p + 1) & 1, t_lo, t_hi);
+      }
+      if (p >= 1) flush((p - 1) & 1, (p - 1) * kJ);
+      refill(pub);
+      s_fill[((p + 1) & 1) * 64 + lane] = fill_end;  // read by the decoder right after B_{p+1}
+      __syncthreads();  // B_{p+1}
+    }
+    if (nph > 0) flush((nph - 1) & 1, (nph - 1) * kJ);
+    return;
+  }
+
+  // ---- decoder. Each phase's kJ records are read into registers at its start (one LDS wait per
+  // phase); the symbol loop is unrolled so every later LDS read on the chain is an explicit
+  // ds_read (ring reads and global fallbacks are separate loads, never one generic pointer).
+  const uint32_t* const L = (const uint32_t*)lds;
+  int valid_end = s_fill[lane];  // ring words readable in this phase
+  auto word = [&](int w) -> uint32_t {
+    uint32_t v = s_ring[((unsigned)w & (kR - 1)) * 64 + lane];
+    if (w >= valid_end) v = bload(r_packed, (uint32_t)(w0 + w) * 4u);
+    return v;
+  };
+  bool ok = live && nw >= 2;
+  uint64_t x = 0;
+  int pos = 0;
+  if (ok) {
+    x = (uint64_t)word(0) | ((uint64_t)word(1) << 32);
+    pos = 2;
+  }
+  uint32_t wnext = pos < nw ? word(pos) : 0u;
   auto renorm = [&]() {
     if (x < kRansL) {
-      if (ptr >= end) return false;
+      if (pos >= nw) return false;
       x = (x << 32) | wnext;
-      ++ptr;
-      wnext = ptr < end ? *ptr : 0u;
+      ++pos;
+      wnext = pos < nw ? word(pos) : 0u;
     }
     return true;
   };
-  const uint64_t mask = (1ull << kPrec) - 1;
-  const int64_t b = live ? sym_off[s] : 0;
-  const int64_t e = live ? sym_off[s + 1] : 0;
-  // all lanes walk the same number of steps (the wave's longest stream); shorter ones idle
-  int64_t len = e - b, maxlen = len;
-  for (int o = 32; o > 0; o >>= 1) {
-    const int64_t v = __shfl_xor(maxlen, o, 64);
-    maxlen = v > maxlen ? v : maxlen;
-  }
-  int32_t cur[kPf], nxt[kPf], off[kPf];
+  const uint32_t mask = (1u << kPrec) - 1;
+  for (int p = 0; p < nph; ++p) {
+    const int buf = p & 1;
+    uint4 rec[kJ];
 #pragma unroll
-  for (int k = 0; k < kPf; ++k) cur[k] = k < len ? indexes[b + k] : 0;
+    for (int j = 0; j < kJ; ++j) rec[j] = s_rec[(buf * kJ + j) * 64 + lane];
 #pragma unroll
-  for (int k = 0; k < kPf; ++k) off[k] = offsets[cur[k]];
-  auto flush = [&](int64_t base, int n) {  // symbols [base, base+n) of this lane from the ring
-    for (int j = 0; j < n; ++j)
-      if (base + j < len) symbols[b + base + j] = ring[j * 64 + lane];
-  };
-  for (int64_t i = 0; i < maxlen; i += kPf) {
-#pragma unroll
-    for (int k = 0; k < kPf; ++k) nxt[k] = i + kPf + k < len ? indexes[b + i + kPf + k] : 0;
-#pragma unroll
-    for (int k = 0; k < kPf; ++k) {
-      const int64_t ik = i + k;
-      const int32_t ci = cur[k];
+    for (int j = 0; j < kJ; ++j) {
+      const uint4 cur = rec[j];
       int32_t value = 0;
-      if (ik < len && ok) {
-        const uint32_t cum = (uint32_t)(x & mask);
-        const uint32_t* sfc = sft + (size_t)ci * cdf_stride;
-        int32_t sidx = lut[(size_t)ci * kLutN + (cum >> kLutShift)];
-        uint32_t sf = sfc[sidx];
-        while (cum >= (sf & 0xFFFFu) + (sf >> 16)) sf = sfc[++sidx];
+      if (p * kJ + j < len && ok) {
+        const int32_t c = (int32_t)cur.x;
+        const uint32_t cum = (uint32_t)x & mask;
+        const bool glob = (cur.z & kGlobTab) != 0u;
+        const uint32_t tb = cur.z & ~kGlobTab;
+        auto tword = [&](uint32_t i) -> uint32_t {  // word i of the table image
+          uint32_t v = L[glob ? 0u : tb + i];
+          if (glob) v = bload(r_img, (tb + i) * 4u);
+          return v;
+        };
+        uint2 ent;
+        if (!glob) {
+          ent = *reinterpret_cast<const uint2*>(L + tb + 2 * (cum >> kL2Shift));
+        } else {
+          ent.x = bload(r_img, (tb + 2 * (cum >> kL2Shift)) * 4u);
+          ent.y = bload(r_img, (tb + 2 * (cum >> kL2Shift) + 1) * 4u);
+        }
+        int32_t sidx = (int32_t)(ent.x & 0xFFFFu);
+        uint32_t sf = ent.y;
+        int hi = (int32_t)(ent.x >> 16);
+        if (hi != sidx) {  // bucket spans symbols sidx .. hi
+          while (sidx < hi) {
+            const int mid = (sidx + hi + 1) >> 1;
+            if ((tword(kL2Words + mid) & 0xFFFFu) <= cum) sidx = mid; else hi = mid - 1;
+          }
+          sf = tword(kL2Words + sidx);
+        }
         const uint32_t start = sf & 0xFFFFu, freq = sf >> 16;
-        x = freq * (x >> kPrec) + cum - start;
+        x = (uint64_t)freq * (x >> kPrec) + (cum - start);
         ok = renorm();
         value = sidx;
         if (ok && start + freq == (1u << kPrec)) {  // escape bin (== max_value)
@@ -391,27 +575,23 @@ __global__ __launch_bounds__(64) void k_rans_decode(
           }
           if (nb > 8) ok = false;
           uint32_t raw = 0;
-          for (int32_t j = 0; ok && j < nb; ++j) {
+          for (int32_t t = 0; ok && t < nb; ++t) {
             ok = getbits(v);
-            raw |= (uint32_t)v << (j * kBypassPrec);
+            raw |= (uint32_t)v << (t * kBypassPrec);
           }
-          const int32_t max_value = cdf_sizes[ci] - 2;
+          const int32_t max_value = cdf_sizes[c] - 2;
           value = (int32_t)(raw >> 1);
           if (raw & 1) value = -value - 1;
           else value += max_value;
         }
-        value += off[k];
+        value += (int32_t)cur.y;
       }
-      ring[(int)(ik % kRing) * 64 + lane] = value;
+      s_out[(buf * kJ + j) * 64 + lane] = value;
     }
-    if ((i + kPf) % kRing == 0) flush(i + kPf - kRing, kRing);
-#pragma unroll
-    for (int k = 0; k < kPf; ++k) cur[k] = nxt[k];
-#pragma unroll
-    for (int k = 0; k < kPf; ++k) off[k] = offsets[cur[k]];
+    s_pos[lane] = pos;  // pos(B_{p+1})
+    __syncthreads();    // B_{p+1}
+    valid_end = s_fill[((p + 1) & 1) * 64 + lane];  // wnext stays valid: unconsumed words stay put
   }
-  const int64_t done = (maxlen + kPf - 1) / kPf * kPf;  // steps written to the ring
-  if (done % kRing) flush(done - done % kRing, (int)(done % kRing));
   if (live) status[s] = ok ? 0 : FVC_ECORRUPT;
 }
 
@@ -514,17 +694,18 @@ int fvc_rans_encode(const int32_t* symbols, const int32_t* indexes, const int64_
 
 size_t fvc_rans_lut_bytes(int ntables, int cdf_stride) {
   if (ntables <= 0 || cdf_stride <= 1) return 0;
-  return (size_t)ntables * ((size_t)cdf_stride * 4 + (size_t)kLutN * 2);
+  return ((size_t)ntables + 1) * 4 + (size_t)ntables * ((size_t)cdf_stride + 1 + kL2Words) * 4;
 }
 
+// layout of the decode-table buffer: img_off [ntables + 1] u32 | img (compact images, k_build_img)
 int fvc_rans_build_lut(const int32_t* cdfs, int cdf_stride, const int32_t* cdf_sizes, int ntables, void* lut,
                        fvc_stream_t s) {
   if (!cdfs || !cdf_sizes || !lut || ntables <= 0 || cdf_stride <= 1) return FVC_EINVAL;
-  uint32_t* sf = (uint32_t*)lut;
-  uint16_t* lut16 = (uint16_t*)(sf + (size_t)ntables * cdf_stride);
-  const size_t n = (size_t)ntables * (kLutN + cdf_stride);
-  hipLaunchKernelGGL(k_build_lut, dim3(grid_for(n)), dim3(kBlk), 0, (hipStream_t)s, cdfs, cdf_stride, cdf_sizes,
-                     ntables, lut16, sf);
+  uint32_t* img_off = (uint32_t*)lut;
+  hipLaunchKernelGGL(k_build_img_off, dim3(1), dim3(64), 0, (hipStream_t)s, cdf_sizes, ntables, img_off);
+  FVC_CHECK_LAUNCH();
+  hipLaunchKernelGGL(k_build_img, dim3(fvc_cdiv(cdf_stride + kL2N, kBlk), ntables), dim3(kBlk), 0,
+                     (hipStream_t)s, cdfs, cdf_stride, cdf_sizes, ntables, img_off, img_off + ntables + 1);
   FVC_CHECK_LAUNCH();
   return 0;
 }
@@ -546,11 +727,11 @@ int fvc_rans_decode(const uint32_t* packed, const int64_t* pack_off, const int32
   if (!packed || !pack_off || !indexes || !sym_off || !cdf_sizes || !offsets || !lut || !symbols || !status ||
       nstreams <= 0 || ntables <= 0 || cdf_stride <= 1)
     return FVC_EINVAL;
-  const uint32_t* sf = (const uint32_t*)lut;
-  const uint16_t* lut16 = (const uint16_t*)(sf + (size_t)ntables * cdf_stride);
-  const int blk = 64;
-  hipLaunchKernelGGL(k_rans_decode, dim3((nstreams + blk - 1) / blk), dim3(blk), 0, (hipStream_t)s, packed, pack_off,
-                     indexes, sym_off, nstreams, cdf_stride, cdf_sizes, offsets, lut16, sf, symbols, status);
+  const uint32_t* img_off = (const uint32_t*)lut;
+  (void)hipFuncSetAttribute((const void*)k_rans_decode, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kDec2Lds);
+  hipLaunchKernelGGL(k_rans_decode, dim3((nstreams + 63) / 64), dim3(128), kDec2Lds, (hipStream_t)s, packed, pack_off,
+                     indexes, sym_off, nstreams, cdf_sizes, offsets, ntables, img_off, img_off + ntables + 1, symbols,
+                     status);
   FVC_CHECK_LAUNCH();
   return 0;
 }

@@ -86,7 +86,10 @@ struct X3Args {
   int ps;                          // LDS plane stride (halves): 8 x (pixels rounded to 8 mod 16)
   unsigned y_bytes;                // bytes of y (and res): < 4 GB - 4 KB, the buffer range
   unsigned x_bytes;                // bytes of one input image: < 4 GB - 4 KB
-  int xcd;                         // XCD-aware mapping of blocks to tile runs
+  int xcd;                         // XCD-aware mapping of blocks to tile runs (static schedule)
+  int* sched;                      // dynamic schedule (may be null: static runs): sched[0] = blocks
+                                   // finished, sched[1 + y * B + z] = next work item of group (y, z);
+                                   // zero on entry, reset to zero by the last block
   int prio;                        // static priority 1 for the second-dispatched half (waves 4-7)
   int* ovf;                        // caller's overflow flag (device int; may be null)
   int toff[4][kMaxTapsX + 1];      // LDS offset (halves) of each tap's window; 0 past ntaps
@@ -148,10 +151,11 @@ __global__ __launch_bounds__(NWV * 64) void conv_x3_kernel(const X3Args a) {
   _Float16* const tile0 = smh + 512;  // two buffers at tile0 and tile0 + tile_h (LDS pointers;
                                       // no pointer array, which would degrade them to flat)
   // LDS header (1 KB): bias of this block's N-tiles [WN * 32] floats at bytes 0..511, the staging
-  // sink at 512..543
+  // sink at 512..543, the work-item queue at 576..591
   float* const sbias = reinterpret_cast<float*>(smh);
   static_assert(WG * WN * 32 * 4 <= 512, "bias area");
   _Float16* const sdump = smh + 256;  // 32 B sink for staging writes of items past the tile
+  int* const squeue = reinterpret_cast<int*>(smh) + 144;  // item k of this block at squeue[k & 3]
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -167,20 +171,47 @@ __global__ __launch_bounds__(NWV * 64) void conv_x3_kernel(const X3Args a) {
   // and every block gets the same mix of 4- / 2- / 1-tap classes); the staging pipeline runs on
   // across item boundaries
   const int nitems = ntiles * a.nclass;
-  // XCD-aware run assignment (a.xcd): consecutive block ids are dispatched round-robin to the 8
-  // XCDs, so logical run lb = (b % 8)-major gives each XCD's blocks one contiguous band of the
-  // image: neighbouring runs share halo rows (and all runs share weights) in that XCD's L2.
-  // Bijective for any grid size (q = G/8, r = G%8: the first r XCDs get q+1 runs).
+  // Work items are taken from the group's counter (a.sched: dynamic schedule; a block that
+  // starts late -- its CU held by another stream's kernel -- just takes fewer items), or as a
+  // static contiguous run per block. The queue holds items k .. k+2 of this block: item k+2 is
+  // taken (one atomic by thread 0) when item k starts and published at the end of its first
+  // chunk, so item k+1 is in LDS before its chunk 0 is staged during item k's last chunk.
+  // Static runs are XCD-aware: consecutive block ids are dispatched round-robin to the 8 XCDs,
+  // so logical run lb = (b % 8)-major gives each XCD's blocks one contiguous band of the image.
+  int* const ctr = a.sched ? a.sched + 1 + blockIdx.z * gridDim.y + blockIdx.y : nullptr;
   int lb = blockIdx.x;
   if (a.xcd) {
     const int G = gridDim.x, q8 = G / 8, r8 = G % 8, x8 = lb % 8;
     lb = (x8 < r8 ? x8 * (q8 + 1) : r8 * (q8 + 1) + (x8 - r8) * q8) + lb / 8;
   }
-  const int w_begin = (int)(((long long)nitems * lb) / gridDim.x);
-  const int w_end = (int)(((long long)nitems * (lb + 1)) / gridDim.x);
-  if (w_begin >= w_end) return;
+  const int run_begin = (int)(((long long)nitems * lb) / gridDim.x);
+  const int run_end = (int)(((long long)nitems * (lb + 1)) / gridDim.x);
+  auto take = [&](int k) -> int {  // thread 0 only
+    if (ctr) return atomicAdd(ctr, 1);
+    return run_begin + k < run_end ? run_begin + k : nitems;
+  };
+  auto finish = [&]() {  // every block, once: the last one leaves the schedule zeroed
+    if (ctr && tid == 0) {
+      __threadfence();
+      const int nblk = (int)(gridDim.x * gridDim.y * gridDim.z);
+      if (atomicAdd(a.sched, 1) == nblk - 1) {
+        for (int g = 0; g < (int)(gridDim.y * gridDim.z); ++g) atomicExch(a.sched + 1 + g, 0);
+        atomicExch(a.sched, 0);
+      }
+    }
+  };
+  if (tid == 0) {
+    squeue[0] = take(0);
+    squeue[1] = take(1);
+  }
+  __syncthreads();
+  const int w_first = squeue[0];
+  if (w_first >= nitems) {
+    finish();
+    return;
+  }
   const int nt0 = blockIdx.y * (WG * WN);  // first N-tile of the block
-  int cls = w_begin % a.nclass;
+  int cls = w_first % a.nclass;
   int nq = a.nks[cls];
   const int hf = a.half;
   const int nch = a.nchunks;
@@ -236,7 +267,7 @@ __global__ __launch_bounds__(NWV * 64) void conv_x3_kernel(const X3Args a) {
 
   for (int e = tid; e < tile_items; e += NT) {
     Stage st;
-    fetch(e, w_begin / a.nclass, 0, st);
+    fetch(e, w_first / a.nclass, 0, st);
     store(tile0, st);
   }
   if (tid < WG * WN * 32) {
@@ -267,9 +298,13 @@ __global__ __launch_bounds__(NWV * 64) void conv_x3_kernel(const X3Args a) {
       __builtin_amdgcn_make_buffer_rsrc((void*)a.y, (short)0, (int)a.y_bytes, kRsrcFlags);
   const __amdgpu_buffer_rsrc_t rr =
       __builtin_amdgcn_make_buffer_rsrc((void*)a.res, (short)0, (int)a.y_bytes, kRsrcFlags);
-  for (int w = w_begin; w < w_end; ++w) {
+  for (int k = 0;; ++k) {
+    const int w = squeue[k & 3];
+    if (w >= nitems) break;
+    int taken = 0;
+    if (tid == 0) taken = take(k + 2);
     const int tile = w / a.nclass;
-    if (w != w_begin) {
+    if (k != 0) {
       cls = w % a.nclass;
       nq = a.nks[cls];
       wcls = a.w + a.wcls[cls];
@@ -295,10 +330,10 @@ __global__ __launch_bounds__(NWV * 64) void conv_x3_kernel(const X3Args a) {
       const _Float16* cur = tile0 + buf * tile_h;
       _Float16* nxt = tile0 + (buf ^ 1) * tile_h;
       const bool last = ch + 1 == nch;
-      const int s_item = last ? w + 1 : w;
+      const int s_item = last ? squeue[(k + 1) & 3] : w;
       const int s_tile = s_item / a.nclass;
       const int s_ch = last ? 0 : ch + 1;
-      const bool stage_next = s_item < w_end;
+      const bool stage_next = s_item < nitems;
       const uint4* wch = wcls + (size_t)ch * nq * a.ntp * kFrag;
       // k-step q: lane half lh takes k8-block kb = 2q + lh = (tap kb / C8, octet kb % C8)
       auto load = [&](int q, Ops& op) {
@@ -402,6 +437,7 @@ __global__ __launch_bounds__(NWV * 64) void conv_x3_kernel(const X3Args a) {
           store(nxt, st);
         }
       }
+      if (ch == 0 && tid == 0) squeue[(k + 2) & 3] = taken;
       __syncthreads();
       buf ^= 1;
     }
@@ -469,6 +505,7 @@ __global__ __launch_bounds__(NWV * 64) void conv_x3_kernel(const X3Args a) {
     }
   }
   if (!(mx < 65000.f) && a.ovf) atomicOr(a.ovf, 1);
+  finish();
 }
 
 // ------------------------------------------------------------------ host-side geometry
@@ -653,7 +690,8 @@ static int x3_launch_cc(int nwv, int wm, int wn, int wg, int iop, int post, cons
 
 static int run_x3(const float* x, const void* wpack, float osc, const float* bias, const float* res,
                   float* y, int batch, int h, int w, int cin, int cout, int ks, int stride, int transposed,
-                  int in_op, int act, int post_op, int cu_reserve, int* ovf, hipStream_t s) {
+                  int in_op, int act, int post_op, int cu_reserve, int* ovf, int* sched, int sched_len,
+                  hipStream_t s) {
   X3Cfg c;
   if (!x3_cfg(cin, cout, ks, stride, transposed, c)) return FVC_EINVAL;
   if (!x || !wpack || !bias || !y || batch <= 0 || h <= 0 || w <= 0) return FVC_EINVAL;
@@ -679,10 +717,10 @@ static int run_x3(const float* x, const void* wpack, float osc, const float* bia
     const int b1 = batch / 2;
     const size_t xs = (size_t)h * w * c.cinp, ys = (size_t)a.Ho * a.Wo * a.coutp;
     int rc = run_x3(x, wpack, osc, bias, res, y, b1, h, w, cin, cout, ks, stride, transposed, in_op, act,
-                    post_op, cu_reserve, ovf, s);
+                    post_op, cu_reserve, ovf, sched, sched_len, s);
     if (rc) return rc;
     return run_x3(x + b1 * xs, wpack, osc, bias, res ? res + b1 * ys : nullptr, y + b1 * ys, batch - b1, h, w, cin, cout, ks,
-                  stride, transposed, in_op, act, post_op, cu_reserve, ovf, s);
+                  stride, transposed, in_op, act, post_op, cu_reserve, ovf, sched, sched_len, s);
   }
   a.y_bytes = (unsigned)ybytes;
   // the input is addressed per image (blockIdx.z) through a 32-bit-range descriptor too
@@ -760,6 +798,8 @@ static int run_x3(const float* x, const void* wpack, float osc, const float* bia
   if (gx > (long long)tiles_x * tiles_y * c.nclass) gx = (long long)tiles_x * tiles_y * c.nclass;
   if (gx < 1) gx = 1;
   dim3 grid((unsigned)gx, c.ntp / nb, batch);
+  // dynamic schedule when the caller's scratch holds the group counters (FVC_X3_DYN=0: static runs)
+  a.sched = (sched && sched_len >= 1 + (long long)grid.y * grid.z && env_int("FVC_X3_DYN", 1)) ? sched : nullptr;
   switch (c.cc) {
     case 8: return x3_launch_cc<8>(c.nw, wm, wn, wg, in_op, post_op, a, grid, lds, s);
     case 16: return x3_launch_cc<16>(c.nw, wm, wn, wg, in_op, post_op, a, grid, lds, s);
@@ -822,19 +862,19 @@ int fvc_conv_x3_pack_weight(const float* w, void* wp, float* osc_out, int cin, i
 int fvc_conv2d_nhwc_x3(const float* x, const void* wpack, float osc, const float* bias,
                        const float* res, float* y, int batch, int h, int w, int cin, int cout,
                        int ksize, int stride, int in_op, int act, int post_op, int cu_reserve,
-                       int* overflow_flag, fvc_stream_t stream) {
-  if (cu_reserve < 0) return FVC_EINVAL;
+                       int* overflow_flag, int* sched, int sched_len, fvc_stream_t stream) {
+  if (cu_reserve < 0 || sched_len < 0) return FVC_EINVAL;
   return run_x3(x, wpack, osc, bias, res, y, batch, h, w, cin, cout, ksize, stride, 0, in_op, act,
-                post_op, cu_reserve, overflow_flag, (hipStream_t)stream);
+                post_op, cu_reserve, overflow_flag, sched, sched_len, (hipStream_t)stream);
 }
 
 int fvc_deconv2d_nhwc_x3(const float* x, const void* wpack, float osc, const float* bias,
                          const float* res, float* y, int batch, int h, int w, int cin, int cout,
                          int ksize, int stride, int in_op, int act, int post_op, int cu_reserve,
-                         int* overflow_flag, fvc_stream_t stream) {
-  if (cu_reserve < 0) return FVC_EINVAL;
+                         int* overflow_flag, int* sched, int sched_len, fvc_stream_t stream) {
+  if (cu_reserve < 0 || sched_len < 0) return FVC_EINVAL;
   return run_x3(x, wpack, osc, bias, res, y, batch, h, w, cin, cout, ksize, stride, 1, in_op, act,
-                post_op, cu_reserve, overflow_flag, (hipStream_t)stream);
+                post_op, cu_reserve, overflow_flag, sched, sched_len, (hipStream_t)stream);
 }
 
 }  // extern "C"

@@ -185,6 +185,18 @@ def cu_reserve(n: int):
 
 
 _OVF = {}
+_SCHED = {}
+SCHED_LEN = 4096
+
+
+def sched_scratch(device=None) -> torch.Tensor:
+    """The x3 conv's dynamic-schedule counters (device int32[SCHED_LEN], zero between launches) of
+    the current stream of device: launches on one stream are ordered, so they can share it."""
+    st = torch.cuda.current_stream(device)
+    key = (str(st.device), st.cuda_stream)
+    if key not in _SCHED:
+        _SCHED[key] = torch.zeros(SCHED_LEN, dtype=torch.int32, device=st.device)
+    return _SCHED[key]
 
 
 def overflow_flag(device=None) -> torch.Tensor:
@@ -301,7 +313,8 @@ class PackedConv:
             fn = "fvc_deconv2d_nhwc_x3" if self.transposed else "fvc_conv2d_nhwc_x3"
             _lib.call(fn, x.data_ptr(), self.wpack.data_ptr(), self.osc, self.bias.data_ptr(), _ptr(res),
                       y.data_ptr(), B, H, W, self.cin, self.cout, self.ksize, self.stride, in_op, act, post,
-                      _STATE["cu_reserve"], overflow_flag(x.device).data_ptr(), stream_handle())
+                      _STATE["cu_reserve"], overflow_flag(x.device).data_ptr(), sched_scratch(x.device).data_ptr(),
+                      SCHED_LEN, stream_handle())
         else:
             fn = "fvc_deconv2d_nhwc_f32" if self.transposed else "fvc_conv2d_nhwc_f32"
             _lib.call(fn, x.data_ptr(), self.wpack.data_ptr(), self.bias.data_ptr(), _ptr(res), y.data_ptr(), B, H,

@@ -86,7 +86,12 @@ int fvc_deconv2d_nhwc_f32(const float* x, const float* wpack, const float* bias,
  * leaves to kernels of other streams (capped at half the CUs). A pipelined caller (encoder +
  * coder + decoder streams in flight, fastvideocodec_amd/gop.py) passes it so that a conv block
  * never waits for a CU held by a long-running rANS chain, which would double that launch's
- * time; 0 = the whole GPU. */
+ * time; 0 = the whole GPU. sched (may be NULL): caller-owned device scratch of sched_len ints,
+ * zero before the first launch, used and left zeroed by each launch (launches sharing it must
+ * be ordered, e.g. one buffer per stream): with at least 1 + (N-groups x batch) ints, blocks take
+ * work items from per-group counters, so a block that starts late (its CU busy with another
+ * stream's kernel) takes fewer tiles instead of stretching the launch; otherwise each block of
+ * the persistent grid walks a fixed run. */
 int fvc_conv_x3_supported(int cin, int cout, int ksize, int stride, int transposed);
 size_t fvc_conv_x3_wpack_bytes(int cin, int cout, int ksize, int stride, int transposed);
 int fvc_conv_x3_pack_weight(const float* w_host, void* wpack_host, float* osc_out, int cin,
@@ -94,11 +99,11 @@ int fvc_conv_x3_pack_weight(const float* w_host, void* wpack_host, float* osc_ou
 int fvc_conv2d_nhwc_x3(const float* x, const void* wpack, float osc, const float* bias,
                        const float* res, float* y, int batch, int h, int w, int cin, int cout,
                        int ksize, int stride, int in_op, int act, int post_op, int cu_reserve,
-                       int* overflow_flag, fvc_stream_t stream);
+                       int* overflow_flag, int* sched, int sched_len, fvc_stream_t stream);
 int fvc_deconv2d_nhwc_x3(const float* x, const void* wpack, float osc, const float* bias,
                          const float* res, float* y, int batch, int h, int w, int cin, int cout,
                          int ksize, int stride, int in_op, int act, int post_op, int cu_reserve,
-                         int* overflow_flag, fvc_stream_t stream);
+                         int* overflow_flag, int* sched, int sched_len, fvc_stream_t stream);
 
 /* ------------------------------------------------------------------ layout / resampling */
 int fvc_nchw_to_nhwc(const float* src, float* dst, int batch, int c, int h, int w, int cp,
@@ -205,8 +210,9 @@ int fvc_rans_pack(const uint32_t* words, const int64_t* word_off, const int32_t*
                   int nstreams, int64_t* pack_off, uint32_t* out, int32_t* status,
                   fvc_stream_t stream);
 /* Decode tables, built once per table set (fvc_rans_lut_bytes(ntables, cdf_stride) bytes): per
- * table a 4096-bucket cum -> first-candidate-symbol map and a start|freq<<16 word per symbol
- * (L2-resident; a decoded symbol costs two dependent cache hits). */
+ * table a 128-bucket cum -> {first, last candidate symbol, start|freq of the first} map and a
+ * start|freq<<16 word per symbol. The decoder copies the tables its streams use into LDS (a
+ * decoded symbol then costs one LDS read in most buckets) and reads the rest from L2. */
 size_t fvc_rans_lut_bytes(int ntables, int cdf_stride);
 int fvc_rans_build_lut(const int32_t* cdfs, int cdf_stride, const int32_t* cdf_sizes, int ntables,
                        void* lut, fvc_stream_t stream);
