@@ -64,6 +64,15 @@ _SIGS = {
     "fvc_iframe_quant": (c_int, [vp, c_int, c_int, c_int, c_int, c_int, c_int, vp]),
     "fvc_iframe_block_index": (c_int, [vp, vp, c_int, vp, vp, c_int, c_int, c_int, c_int, vp]),
     "fvc_iframe_expand_index": (c_int, [vp, vp, c_int, c_int, c_int, c_int, vp]),
+    "fvc_torchac_normalize": (c_int, [vp, ctypes.c_int64, c_int, c_int, vp, vp]),
+    "fvc_torchac_rows_bounds": (c_int, [vp, vp, ctypes.c_int64, c_int, vp, vp, vp, vp]),
+    "fvc_torchac_laplace_rows": (c_int, [vp] + [c_int] * 6 + [vp, vp]),
+    "fvc_torchac_laplace_bounds": (c_int, [vp, vp] + [c_int] * 6 + [vp, vp, vp, vp]),
+    "fvc_torchac_bitest_table": (c_int, [vp, c_int, c_int, vp, vp]),
+    "fvc_torchac_table_bounds": (c_int, [vp, vp] + [c_int] * 6 + [vp, vp, vp, vp]),
+    "fvc_torchac_max_bytes": (c_size_t, [ctypes.c_int64]),
+    "fvc_torchac_encode": (c_int, [vp, vp, ctypes.c_int64, vp, c_size_t, vp]),
+    "fvc_torchac_decode": (c_int, [vp, c_int, vp, ctypes.c_int64, ctypes.c_int64, vp, c_size_t, vp]),
 }
 
 EXPORTED = tuple(_SIGS)

@@ -10,10 +10,11 @@ import sys
 from concurrent.futures import ThreadPoolExecutor
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-SRCS = ["fvc_conv.hip", "fvc_conv_x3.hip", "fvc_elem.hip", "fvc_coder.hip", "fvc_iframe.hip"]
+SRCS = ["fvc_conv.hip", "fvc_conv_x3.hip", "fvc_elem.hip", "fvc_coder.hip", "fvc_iframe.hip", "fvc_torchac.hip"]
 OUT = os.path.join(HERE, "libfvc.so")
 OBJDIR = os.path.join(HERE, "build")
-HEADERS = [os.path.join(HERE, "csrc", "fvc_common.h"), os.path.join(os.path.dirname(HERE), "include", "fvc.h")]
+HEADERS = [os.path.join(HERE, "csrc", "fvc_common.h"), os.path.join(HERE, "csrc", "fvc_dist.h"),
+           os.path.join(os.path.dirname(HERE), "include", "fvc.h")]
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Wno-unused-result"]
 
 

@@ -5,6 +5,7 @@
 // contraction off (no FMA fusion) and in the reference's operand order, so results track the
 // CPU path to ~1 ulp.
 #include "fvc_common.h"
+#include "fvc_dist.h"
 #include <string.h>
 
 #pragma clang fp contract(off)
@@ -446,10 +447,7 @@ __global__ __launch_bounds__(kBlk) void k_recon_finalize(const float* __restrict
 }
 
 // Laplace bits (net.py:121-151): p = cdf(f+.5) - cdf(f-.5), cdf(v) = .5 - .5 sign(v) expm1(-|v|/s)
-__device__ __forceinline__ float laplace_cdf(float v, float s) {
-  const float sg = v > 0.f ? 1.f : (v < 0.f ? -1.f : 0.f);
-  return 0.5f - 0.5f * sg * expm1f(-fabsf(v) / s);
-}
+__device__ __forceinline__ float laplace_cdf(float v, float s) { return fvc_laplace_cdf(v, s); }
 
 __device__ __forceinline__ float bits_of_prob(float p) {
   float b = -1.0f * logf(p + 1e-5f) / 0.6931471805599453f;
@@ -471,18 +469,8 @@ __global__ __launch_bounds__(kBlk) void k_bits_laplace(const float* __restrict__
   block_reduce_store<1>(acc, ws);
 }
 
-__device__ __forceinline__ float softplus_f(float v) { return v > 20.f ? v : log1pf(expf(v)); }
-
 __device__ __forceinline__ float bitest_cdf(float x, const float* prm, int C, int c) {
-#pragma unroll
-  for (int f = 0; f < 3; ++f) {
-    const float h = prm[(3 * f) * C + c], b = prm[(3 * f + 1) * C + c], a = prm[(3 * f + 2) * C + c];
-    x = x * softplus_f(h) + b;
-    x = x + tanhf(x) * tanhf(a);
-  }
-  const float h = prm[9 * C + c], b = prm[10 * C + c];
-  const float t = x * softplus_f(h) + b;
-  return 1.f / (1.f + expf(-t));
+  return fvc_bitest_cdf(x, prm, C, c);
 }
 
 __global__ __launch_bounds__(kBlk) void k_bits_factorized(const float* __restrict__ v, const float* __restrict__ prm,

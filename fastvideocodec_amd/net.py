@@ -24,6 +24,7 @@ import torch.nn as nn
 from torch.nn import Parameter
 
 from . import kernels as K
+from . import torchac as TAC
 from ._lib import FvcError
 from .entropy_models import FactorizedTables, LaplaceTables, RangeCoder, get_scale_table
 from .weights import OUT_CHANNEL_M, OUT_CHANNEL_MV, OUT_CHANNEL_N
@@ -453,10 +454,15 @@ class VideoCompressor(nn.Module):
         clipped, sse = K.recon_finalize(t["recon"], t["cur4"], t["warpframe"], t["prediction"])
         npx = B * H * W
         if self.calrealbits:
-            bs = self.compress_tensors(t)
-            bits_f = bs.feature.pack_off[-1:].double() * 32
-            bits_z = bs.z.pack_off[-1:].double() * 32
-            bits_mv = bs.mv.pack_off[-1:].double() * 32
+            # DVC's real-bits mode (net.py:123-205): lengths of the torchac byte strings of the three
+            # latents (one string per tensor, 2*mxrange-bin CDF rows), from the torchac-compatible
+            # coder (torchac.py)
+            bz, bmv = self._be_params()
+            lens = (TAC.laplace_encode(t["feature"], t["sigma"], OUT_CHANNEL_M, self.mxrange),
+                    TAC.bitest_encode(t["z"], bz, OUT_CHANNEL_N, self.mxrange),
+                    TAC.bitest_encode(t["mvfeature"], bmv, OUT_CHANNEL_MV, self.mxrange))
+            bits_f, bits_z, bits_mv = (torch.tensor([8.0 * len(s)], dtype=torch.float64, device=input_image.device)
+                                       for s in lens)
         else:
             bz, bmv = self._be_params()
             bits_f = K.bits_laplace(t["feature"], t["sigma"], OUT_CHANNEL_M)

@@ -248,6 +248,32 @@ int fvc_iframe_block_index(const int32_t* coeff, const float* scale_table, int n
 int fvc_iframe_expand_index(const uint8_t* bidx, int32_t* idx, int planes, int h, int w, int bs,
                             fvc_stream_t stream);
 
+/* ------------------------------------------------------------------ torchac-compatible coder
+ * Replaces torchac.encode_float_cdf / decode_float_cdf (third-party, absent), which DVC's
+ * calrealbits mode calls with 2*mxrange bins per element (DVC/net.py:123-138, 155-168, 183-195).
+ * Device (stream-ordered): CDF rows / symbol bounds in torchac's int16 normalisation
+ * (round(cdf * (2^16 - (Lp-1))) + k, as uint16), elements in NCHW order; latents are NHWC with
+ * cp padded channels. status (device int) |= 1 for a symbol outside [0, Lp-2] (torchac's
+ * check_input_bounds). Host (synchronous, CPU memory): the sequential arithmetic coder over
+ * [lo, hi) bounds (encode: FVC_ENOSPC if cap is too small; fvc_torchac_max_bytes(n) always
+ * fits) and its decoder over uint16 rows (rows == NULL: element i uses row i; else rows[i] < nrows). */
+int fvc_torchac_normalize(const float* cdf, int64_t nrows, int Lp, int needs_normalization, uint16_t* out,
+                          fvc_stream_t stream);
+int fvc_torchac_rows_bounds(const uint16_t* rows, const int16_t* sym, int64_t n, int Lp, uint32_t* lo,
+                            uint32_t* hi, int* status, fvc_stream_t stream);
+int fvc_torchac_laplace_rows(const float* sigma, int batch, int h, int w, int c, int cp, int mxrange,
+                             uint16_t* rows, fvc_stream_t stream);
+int fvc_torchac_laplace_bounds(const float* x, const float* sigma, int batch, int h, int w, int c, int cp,
+                               int mxrange, uint32_t* lo, uint32_t* hi, int* status, fvc_stream_t stream);
+int fvc_torchac_bitest_table(const float* params, int c, int mxrange, uint16_t* table, fvc_stream_t stream);
+int fvc_torchac_table_bounds(const float* x, const uint16_t* table, int batch, int h, int w, int c, int cp,
+                             int mxrange, uint32_t* lo, uint32_t* hi, int* status, fvc_stream_t stream);
+size_t fvc_torchac_max_bytes(int64_t n);
+int fvc_torchac_encode(const uint32_t* lo, const uint32_t* hi, int64_t n, uint8_t* out, size_t cap,
+                       size_t* out_len);
+int fvc_torchac_decode(const uint16_t* cdf, int Lp, const int32_t* rows, int64_t nrows, int64_t n,
+                       const uint8_t* in, size_t len, int16_t* sym);
+
 #ifdef __cplusplus
 }
 #endif
