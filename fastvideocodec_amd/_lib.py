@@ -64,6 +64,11 @@ _SIGS = {
     "fvc_iframe_quant": (c_int, [vp, c_int, c_int, c_int, c_int, c_int, c_int, vp]),
     "fvc_iframe_block_index": (c_int, [vp, vp, c_int, vp, vp, c_int, c_int, c_int, c_int, vp]),
     "fvc_iframe_expand_index": (c_int, [vp, vp, c_int, c_int, c_int, c_int, vp]),
+    "fvc_gdn_nhwc_cai": (c_int, [vp, vp, vp, vp] + [c_int] * 5 + [vp]),
+    "fvc_lstm_gates": (c_int, [vp] * 7 + [c_size_t, ctypes.c_float, vp]),
+    "fvc_rpm_scale": (c_int, [vp, vp, c_size_t, vp]),
+    "fvc_eb_forward": (c_int, [vp] * 6 + [c_int] * 5 + [vp]),
+    "fvc_gc_forward": (c_int, [vp] * 6 + [c_int] * 5 + [vp]),
     "fvc_torchac_normalize": (c_int, [vp, ctypes.c_int64, c_int, c_int, vp, vp]),
     "fvc_torchac_rows_bounds": (c_int, [vp, vp, ctypes.c_int64, c_int, vp, vp, vp, vp]),
     "fvc_torchac_laplace_rows": (c_int, [vp] + [c_int] * 6 + [vp, vp]),

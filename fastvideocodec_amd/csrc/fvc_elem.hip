@@ -487,6 +487,162 @@ __global__ __launch_bounds__(kBlk) void k_bits_factorized(const float* __restric
   block_reduce_store<1>(acc, ws);
 }
 
+
+// ------------------------------------------------------------------ RLVC path
+// compressai.layers.GDN (models.py:23,529-538): norm = conv1x1(x^2, gamma) + beta,
+// y = x * rsqrt(norm) (GDN) or x * sqrt(norm) (IGDN), any C (RLVC: 128). A block of C threads
+// walks pixels in groups of kGcPix: the group's x rows go to LDS, thread i keeps row i of gamma
+// in registers and sums gamma[i][j] x_j^2 over the LDS rows (broadcast reads).
+constexpr int kGcPix = 8;
+
+template <int C>
+__global__ __launch_bounds__(C) void k_gdn_cai(const float* __restrict__ x, float* __restrict__ y,
+                                               const float* __restrict__ beta, const float* __restrict__ gamma,
+                                               size_t npix, int inverse) {
+  __shared__ float xs[kGcPix][C];
+  const int i = threadIdx.x;
+  float g[C];
+#pragma unroll
+  for (int j = 0; j < C; ++j) g[j] = gamma[(size_t)i * C + j];
+  const float b = beta[i];
+  for (size_t p0 = (size_t)blockIdx.x * kGcPix; p0 < npix; p0 += (size_t)gridDim.x * kGcPix) {
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < kGcPix; ++q) xs[q][i] = p0 + q < npix ? x[(p0 + q) * C + i] : 0.f;
+    __syncthreads();
+    float acc[kGcPix];
+#pragma unroll
+    for (int q = 0; q < kGcPix; ++q) acc[q] = 0.f;
+#pragma unroll 8
+    for (int j = 0; j < C; ++j) {
+#pragma unroll
+      for (int q = 0; q < kGcPix; ++q) {
+        const float v = xs[q][j];
+        acc[q] = fmaf(g[j], v * v, acc[q]);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < kGcPix; ++q) {
+      if (p0 + q >= npix) break;
+      const float norm = acc[q] + b;
+      const float xv = xs[q][i];
+      y[(p0 + q) * C + i] = inverse ? xv * sqrtf(norm) : xv * (1.f / sqrtf(norm));
+    }
+  }
+}
+
+// ConvLSTM gates (entropy_models.py:367-378): f = sigmoid(f + forget_bias), i = sigmoid(i),
+// c = c * f + i * relu(j), o = sigmoid(o), h = o * relu(c); NHWC tensors of C channels
+__device__ __forceinline__ float sigmoid_t(float v) { return 1.f / (1.f + expf(-v)); }
+
+__global__ void k_lstm_gates(const float* __restrict__ gj, const float* __restrict__ gi, const float* __restrict__ gf,
+                             const float* __restrict__ go, const float* __restrict__ c_prev, float* __restrict__ c_out,
+                             float* __restrict__ h_out, size_t n, float forget_bias) {
+  for (size_t e = grid_stride_start(); e < n; e += (size_t)gridDim.x * blockDim.x) {
+    const float f = sigmoid_t(gf[e] + forget_bias);
+    const float ig = sigmoid_t(gi[e]);
+    const float c = c_prev[e] * f + ig * fmaxf(gj[e], 0.f);
+    const float o = sigmoid_t(go[e]);
+    c_out[e] = c;
+    h_out[e] = o * fmaxf(c, 0.f);
+  }
+}
+
+// RecProbModel sigma (entropy_models.py:61-62): exp(max(sigma, -7)) / 10
+__global__ void k_rpm_scale(const float* __restrict__ in, float* __restrict__ out, size_t n) {
+  for (size_t e = grid_stride_start(); e < n; e += (size_t)gridDim.x * blockDim.x)
+    out[e] = expf(fmaxf(in[e], -7.f)) / 10.f;
+}
+
+__device__ __forceinline__ float bits_lb(float l) {  // likelihood_lower_bound(1e-9), then the bits clamp
+  return bits_of_prob(fmaxf(l, 1e-9f));
+}
+
+// compressai EntropyBottleneck, filters (3,3,3,3) (compressai EB._logits_cumulative): per
+// channel prm[c][kEbPrm] = softplus(matrix0..4) (3, 9, 9, 9, 3), bias0..4 (3, 3, 3, 3, 1),
+// tanh(factor0..3) (3 x 4)
+constexpr int kEbPrm = 58;
+__device__ float eb_logits(float v, const float* __restrict__ p) {
+  const float* m0 = p;
+  const float* m1 = p + 3;
+  const float* m2 = p + 12;
+  const float* m3 = p + 21;
+  const float* m4 = p + 30;
+  const float* bs = p + 33;  // b0[3] b1[3] b2[3] b3[3] b4[1]
+  const float* fs = p + 46;  // f0[3] f1[3] f2[3] f3[3]
+  float a[3], t[3];
+#pragma unroll
+  for (int r = 0; r < 3; ++r) {
+    a[r] = m0[r] * v + bs[r];
+    a[r] += fs[r] * tanhf(a[r]);
+  }
+  const float* ms[3] = {m1, m2, m3};
+#pragma unroll
+  for (int l = 0; l < 3; ++l) {
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      float acc = ms[l][3 * r] * a[0];
+      acc = fmaf(ms[l][3 * r + 1], a[1], acc);
+      acc = fmaf(ms[l][3 * r + 2], a[2], acc);
+      t[r] = acc + bs[3 * (l + 1) + r];
+      t[r] += fs[3 * (l + 1) + r] * tanhf(t[r]);
+    }
+#pragma unroll
+    for (int r = 0; r < 3; ++r) a[r] = t[r];
+  }
+  float o = m4[0] * a[0];
+  o = fmaf(m4[1], a[1], o);
+  o = fmaf(m4[2], a[2], o);
+  return o + bs[12];
+}
+
+// x_hat = round(x - median) + median; likelihood = |sigmoid(s*upper) - sigmoid(s*lower)|,
+// s = -sign(lower + upper) (compressai EB._likelihood); out: x_hat and the bits sum
+__global__ __launch_bounds__(kBlk) void k_eb_forward(const float* __restrict__ x, const float* __restrict__ prm,
+                                                     const float* __restrict__ med, float* __restrict__ xhat,
+                                                     double* __restrict__ ws, size_t npix, int C, int cp) {
+  double acc[1] = {0.0};
+  const size_t n = npix * C;
+  for (size_t e = grid_stride_start(); e < n; e += (size_t)gridDim.x * blockDim.x) {
+    const size_t p = e / C;
+    const int c = (int)(e - p * C);
+    const float m = med[c];
+    const float v = rintf(x[p * cp + c] - m) + m;
+    xhat[p * cp + c] = v;
+    const float lo = eb_logits(v - 0.5f, prm + (size_t)c * kEbPrm);
+    const float up = eb_logits(v + 0.5f, prm + (size_t)c * kEbPrm);
+    const float sum = lo + up;
+    const float sg = sum > 0.f ? -1.f : (sum < 0.f ? 1.f : 0.f);
+    acc[0] += (double)bits_lb(fabsf(sigmoid_t(sg * up) - sigmoid_t(sg * lo)));
+  }
+  block_reduce_store<1>(acc, ws);
+}
+
+// GaussianConditional with means (compressai GC._likelihood): x_hat = round(x - mu) + mu,
+// v = |x_hat - mu|, s = max(scale, 0.11), l = Phi((.5 - v)/s) - Phi((-.5 - v)/s),
+// Phi(t) = .5 erfc(-t / sqrt 2)
+__global__ __launch_bounds__(kBlk) void k_gc_forward(const float* __restrict__ x, const float* __restrict__ scale,
+                                                     const float* __restrict__ mu, float* __restrict__ xhat,
+                                                     double* __restrict__ ws, size_t npix, int C, int cp) {
+  double acc[1] = {0.0};
+  const size_t n = npix * C;
+  const float k = -0.70710678118654752f;  // -(2^-0.5)
+  for (size_t e = grid_stride_start(); e < n; e += (size_t)gridDim.x * blockDim.x) {
+    const size_t p = e / C;
+    const int c = (int)(e - p * C);
+    const size_t o = p * cp + c;
+    const float m = mu[o];
+    const float xh = rintf(x[o] - m) + m;
+    xhat[o] = xh;
+    const float v = fabsf(xh - m);
+    const float s = fmaxf(scale[o], 0.11f);
+    const float up = 0.5f * erfcf(k * ((0.5f - v) / s));
+    const float lo = 0.5f * erfcf(k * ((-0.5f - v) / s));
+    acc[0] += (double)bits_lb(up - lo);
+  }
+  block_reduce_store<1>(acc, ws);
+}
+
 static int grid_for(size_t n) {
   size_t g = (n + kBlk - 1) / kBlk;
   if (g > 8192) g = 8192;
@@ -600,6 +756,61 @@ int fvc_tap_gather_nhwc(const float* P, int pcp, const float* bias, const float*
 int fvc_sub_f32(const float* a, const float* b, float* out, size_t n, fvc_stream_t s) {
   if (!a || !b || !out) return FVC_EINVAL;
   hipLaunchKernelGGL(k_sub, dim3(grid_for(n)), dim3(kBlk), 0, (hipStream_t)s, a, b, out, n);
+  FVC_CHECK_LAUNCH();
+  return 0;
+}
+
+int fvc_gdn_nhwc_cai(const float* x, float* y, const float* beta, const float* gamma, int batch, int h, int w, int c,
+                     int inverse, fvc_stream_t s) {
+  if (!x || !y || !beta || !gamma || (c != 64 && c != 128)) return FVC_EINVAL;
+  const size_t npix = (size_t)batch * h * w;
+  size_t nblk = (npix + kGcPix - 1) / kGcPix;
+  if (nblk > 8192) nblk = 8192;
+  if (nblk < 1) nblk = 1;
+  if (c == 128)
+    hipLaunchKernelGGL(k_gdn_cai<128>, dim3((unsigned)nblk), dim3(128), 0, (hipStream_t)s, x, y, beta, gamma, npix,
+                       inverse);
+  else
+    hipLaunchKernelGGL(k_gdn_cai<64>, dim3((unsigned)nblk), dim3(64), 0, (hipStream_t)s, x, y, beta, gamma, npix,
+                       inverse);
+  FVC_CHECK_LAUNCH();
+  return 0;
+}
+
+int fvc_lstm_gates(const float* gj, const float* gi, const float* gf, const float* go, const float* c_prev,
+                   float* c_out, float* h_out, size_t n, float forget_bias, fvc_stream_t s) {
+  if (!gj || !gi || !gf || !go || !c_prev || !c_out || !h_out) return FVC_EINVAL;
+  hipLaunchKernelGGL(k_lstm_gates, dim3(grid_for(n)), dim3(kBlk), 0, (hipStream_t)s, gj, gi, gf, go, c_prev, c_out,
+                     h_out, n, forget_bias);
+  FVC_CHECK_LAUNCH();
+  return 0;
+}
+
+int fvc_rpm_scale(const float* in, float* out, size_t n, fvc_stream_t s) {
+  if (!in || !out) return FVC_EINVAL;
+  hipLaunchKernelGGL(k_rpm_scale, dim3(grid_for(n)), dim3(kBlk), 0, (hipStream_t)s, in, out, n);
+  FVC_CHECK_LAUNCH();
+  return 0;
+}
+
+int fvc_eb_forward(const float* x, const float* params, const float* medians, float* xhat, double* out1, double* ws,
+                   int batch, int h, int w, int c, int cp, fvc_stream_t s) {
+  if (!x || !params || !medians || !xhat || !out1 || !ws || c > cp) return FVC_EINVAL;
+  hipLaunchKernelGGL(k_eb_forward, dim3(kRedBlocks), dim3(kBlk), 0, (hipStream_t)s, x, params, medians, xhat, ws,
+                     (size_t)batch * h * w, c, cp);
+  FVC_CHECK_LAUNCH();
+  hipLaunchKernelGGL(k_reduce_partials<1>, dim3(1), dim3(kBlk), 0, (hipStream_t)s, ws, kRedBlocks, out1);
+  FVC_CHECK_LAUNCH();
+  return 0;
+}
+
+int fvc_gc_forward(const float* x, const float* scale, const float* mu, float* xhat, double* out1, double* ws,
+                   int batch, int h, int w, int c, int cp, fvc_stream_t s) {
+  if (!x || !scale || !mu || !xhat || !out1 || !ws || c > cp) return FVC_EINVAL;
+  hipLaunchKernelGGL(k_gc_forward, dim3(kRedBlocks), dim3(kBlk), 0, (hipStream_t)s, x, scale, mu, xhat, ws,
+                     (size_t)batch * h * w, c, cp);
+  FVC_CHECK_LAUNCH();
+  hipLaunchKernelGGL(k_reduce_partials<1>, dim3(1), dim3(kBlk), 0, (hipStream_t)s, ws, kRedBlocks, out1);
   FVC_CHECK_LAUNCH();
   return 0;
 }

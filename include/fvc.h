@@ -248,6 +248,26 @@ int fvc_iframe_block_index(const int32_t* coeff, const float* scale_table, int n
 int fvc_iframe_expand_index(const uint8_t* bidx, int32_t* idx, int planes, int h, int w, int bs,
                             fvc_stream_t stream);
 
+/* ------------------------------------------------------------------ RLVC path
+ * gdn_nhwc_cai: compressai.layers.GDN (models.py:23; RLVC Coder2D, models.py:529-538), C in
+ *   {64, 128}: y = x * rsqrt(beta + gamma . x^2), inverse: y = x * sqrt(...); beta/gamma effective.
+ * lstm_gates: ConvLSTM cell update (entropy_models.py:367-378) from the 4 gate conv outputs.
+ * rpm_scale: exp(max(sigma, -7)) / 10 (entropy_models.py:61-62).
+ * eb_forward: compressai EntropyBottleneck (filters 3,3,3,3) eval forward: x_hat = round(x - med)
+ *   + med and the sum of clamp(-log2(likelihood + 1e-5), 0, 50) (get_estimate_bits,
+ *   entropy_models.py:74-78); params [C][58] = softplus(matrices), biases, tanh(factors).
+ * gc_forward: compressai GaussianConditional with means: x_hat = round(x - mu) + mu and the bits
+ *   sum under N(mu, max(scale, 0.11)). */
+int fvc_gdn_nhwc_cai(const float* x, float* y, const float* beta, const float* gamma, int batch, int h, int w,
+                     int c, int inverse, fvc_stream_t stream);
+int fvc_lstm_gates(const float* gj, const float* gi, const float* gf, const float* go, const float* c_prev,
+                   float* c_out, float* h_out, size_t n, float forget_bias, fvc_stream_t stream);
+int fvc_rpm_scale(const float* in, float* out, size_t n, fvc_stream_t stream);
+int fvc_eb_forward(const float* x, const float* params, const float* medians, float* xhat, double* out1,
+                   double* ws, int batch, int h, int w, int c, int cp, fvc_stream_t stream);
+int fvc_gc_forward(const float* x, const float* scale, const float* mu, float* xhat, double* out1, double* ws,
+                   int batch, int h, int w, int c, int cp, fvc_stream_t stream);
+
 /* ------------------------------------------------------------------ torchac-compatible coder
  * Replaces torchac.encode_float_cdf / decode_float_cdf (third-party, absent), which DVC's
  * calrealbits mode calls with 2*mxrange bins per element (DVC/net.py:123-138, 155-168, 183-195).
