@@ -10,6 +10,7 @@ import sys
 from concurrent.futures import ThreadPoolExecutor
 
 HERE = os.path.dirname(os.path.abspath(__file__))
+VARIANT_SRCS = ("fvc_conv_x3.hip",)
 SRCS = ["fvc_conv.hip", "fvc_conv_x3.hip", "fvc_elem.hip", "fvc_coder.hip", "fvc_iframe.hip", "fvc_torchac.hip"]
 OUT = os.path.join(HERE, "libfvc.so")
 OBJDIR = os.path.join(HERE, "build")
@@ -50,11 +51,16 @@ def build(force=False, verbose=True, variant=None, defines=()):
     tag = f"_{variant}" if variant else ""
     out = OUT if not variant else os.path.join(HERE, f"libfvc{tag}.so")
     extra = [f"-D{d}" for d in defines]
-    todo = [s for s in SRCS if force or _stale(_obj(s, tag), [os.path.join(HERE, "csrc", s)] + HEADERS)]
+    # experiment variants recompile only the conv kernels (the -D switches are theirs) and link
+    # the product objects of every other source
+    vsrcs = [s for s in SRCS if not variant or s in VARIANT_SRCS]
+    if variant:
+        build(force=False, verbose=verbose)
+    todo = [s for s in vsrcs if force or _stale(_obj(s, tag), [os.path.join(HERE, "csrc", s)] + HEADERS)]
     if todo:
         with ThreadPoolExecutor(max_workers=min(len(todo), 4)) as ex:
             list(ex.map(lambda s: _compile(s, verbose, extra, tag), todo))
-    objs = [_obj(s, tag) for s in SRCS]
+    objs = [_obj(s, tag if s in vsrcs else "") for s in SRCS]
     if force or todo or _stale(out, objs):
         cmd = [_hipcc(), "--offload-arch=gfx950", "-shared", "-fPIC", "-o", out + ".tmp"] + objs
         if verbose:

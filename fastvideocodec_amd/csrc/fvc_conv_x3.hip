@@ -61,7 +61,25 @@ constexpr float kLoScale = 2048.f;
 #define FVC_X3_KO 0
 #endif
 constexpr int kKO = FVC_X3_KO;  // activation residual scale
-constexpr int kNPL = 2;                    // weight planes per (k-step, N-tile): hi, lo
+// FVC_X3_SCHED (compile-time, experiments): how each half-step's instruction stream is ordered.
+// 0: sched_barrier pins [next operands' loads] then [MFMAs]; 1: compiler's own order within a
+// half-step; 2: sched_group_barrier interleave, one load between consecutive MFMAs
+// (profiles/r2/x3_experiments: 1 and 2 within +-5 % per geometry, 1 -1 % in the pipelined bench)
+#ifndef FVC_X3_SCHED
+#define FVC_X3_SCHED 0
+#endif
+constexpr int kSched = FVC_X3_SCHED;
+// FVC_X3_ACC1 (compile-time variant): one accumulator. The weight pack carries three planes, hi,
+// (w - hi) and hi * 2^-11 (the last two may be fp16 subnormals: their absolute error 2^-25 is
+// 2^-39 of the layer's largest weight, which the pack scales into [2^13, 2^14)), so
+//     acc += hi_w * hi_x + (w - hi)_w * hi_x + (hi_w 2^-11) * (lo_x 2^11)
+// sums the same three products in one fp32 accumulator: half the accumulator registers and one
+// FMA per output in the epilogue, for 1.5x the weight operand bytes.
+#ifndef FVC_X3_ACC1
+#define FVC_X3_ACC1 0
+#endif
+constexpr int kAcc1 = FVC_X3_ACC1;
+constexpr int kNPL = kAcc1 ? 3 : 2;        // weight planes per (k-step, N-tile): hi, lo [, hi 2^-11]
 constexpr int kFrag = 64 * kNPL;          // uint4 per (k-step, N-tile)
 
 struct X3Args {
@@ -92,6 +110,7 @@ struct X3Args {
                                    // zero on entry, reset to zero by the last block
   int prio;                        // static priority 1 for the second-dispatched half (waves 4-7)
   int* ovf;                        // caller's overflow flag (device int; may be null)
+  int wl_h;                        // WL: halves per LDS weight buffer (the chunk's fragments)
   int toff[4][kMaxTapsX + 1];      // LDS offset (halves) of each tap's window; 0 past ntaps
 };
 
@@ -125,6 +144,45 @@ __device__ __forceinline__ void split8(const float (&v)[8], h8& hi, h8& lo, floa
                        fmaxf(fmaxf(fabsf(v[4]), fabsf(v[5])), fmaxf(fabsf(v[6]), fabsf(v[7])))));
 }
 
+// FVC_X3_TRACE (compile-time, diagnostic builds only): per wave, s_memtime sums of the k-loop's
+// segments (0 prologue, 1 operand/staging load issue, 2 MFMA blocks, 3 staging split + LDS write,
+// 4 chunk end: leftover staging + barrier, 5 epilogue, 6 whole wave) into g_x3_trace. Each stamp
+// drains lgkmcnt, so read shares, not lengths.
+#ifndef FVC_X3_TRACE
+#define FVC_X3_TRACE 0
+#endif
+constexpr int kTraceVals = 8;
+constexpr int kTraceSlots = 1 << 16;
+#if FVC_X3_TRACE
+__device__ unsigned long long g_x3_trace[kTraceSlots * kTraceVals];
+#endif
+__device__ __forceinline__ unsigned long long x3_stamp() {
+  unsigned long long t = 0;
+#if FVC_X3_TRACE
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) : : "memory");
+  __builtin_amdgcn_sched_barrier(0);
+#endif
+  return t;
+}
+
+// One 1-KB LDS-DMA piece: lane l's 16 B at g land at LDS byte lds + 16 l. Inline asm (M0 saved
+// and restored around it) so the compiler neither sees an LDS write it must drain with vmcnt(0)
+// before every later ds_read nor counts it: the kernel orders it itself (vmcnt(0) before the
+// barrier that precedes the first read of the buffer it fills).
+__device__ __forceinline__ void glds16(const void* g, unsigned lds) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(g), "s"(lds)
+               : "memory");
+}
+
+__device__ __forceinline__ unsigned lds_addr(const void* p) {
+  return __builtin_amdgcn_readfirstlane(
+      (unsigned)(uintptr_t)((const __attribute__((address_space(3))) char*)p));
+}
+
 // x and y / res are addressed through buffer descriptors with 32-bit offsets (the host keeps
 // each image's input and each launch's output under 4 GB): a halo pixel outside the image gets an
 // offset past the descriptor's range and loads zeros (the conv's zero padding, no select), and a
@@ -137,7 +195,11 @@ constexpr int kRsrcFlags = 0x00020000;
 // WG = 2, WM = 4, WN = 1 a wave re-uses each weight fragment on 4 strips: half the weight bytes
 // per MFMA of WG = 1, WM = 2, WN = 2 through the vector-memory return path (TD), which the PMC
 // passes show as the kernel's binding unit (scripts/gpu_pmc_x3.sh: TD busy 77 % at 40 % MFMA).
-template <int CC, int WM, int WN, int WG, int IOP, int POST, int NWV>
+// WL = 1: the block's weight fragments of each chunk are copied once into LDS by LDS-DMA
+// (global_load_lds, no VGPRs, issued with the chunk's activation staging one chunk ahead) and the
+// waves read them with ds_read_b128 instead of each wave fetching the same 1-KB fragments from L2
+// through the vector-memory return path (8 waves x WN x 2 KB per k-step).
+template <int CC, int WM, int WN, int WG, int IOP, int POST, int NWV, int WL>
 __global__ __launch_bounds__(NWV * 64) void conv_x3_kernel(const X3Args a) {
   constexpr int NW = NWV / WG;       // waves stacked vertically per N-group
   constexpr int C8 = CC / 8;
@@ -150,6 +212,7 @@ __global__ __launch_bounds__(NWV * 64) void conv_x3_kernel(const X3Args a) {
   const int tile_h = 2 * C8 * a.ps;  // halves per A buffer: 2*C8 planes (hi octets, lo octets)
   _Float16* const tile0 = smh + 512;  // two buffers at tile0 and tile0 + tile_h (LDS pointers;
                                       // no pointer array, which would degrade them to flat)
+  _Float16* const wbase = tile0 + 2 * tile_h;  // WL: two weight buffers of a.wl_h halves
   // LDS header (1 KB): bias of this block's N-tiles [WN * 32] floats at bytes 0..511, the staging
   // sink at 512..543, the work-item queue at 576..591
   float* const sbias = reinterpret_cast<float*>(smh);
@@ -157,9 +220,19 @@ __global__ __launch_bounds__(NWV * 64) void conv_x3_kernel(const X3Args a) {
   _Float16* const sdump = smh + 256;  // 32 B sink for staging writes of items past the tile
   int* const squeue = reinterpret_cast<int*>(smh) + 144;  // item k of this block at squeue[k & 3]
 
+  unsigned long long tr[kTraceVals] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long tr_t0 = x3_stamp();
+  const unsigned long long tr_begin = tr_t0;
+  auto TR = [&](int i) {  // close the running segment, attributing it to i
+    if constexpr (FVC_X3_TRACE != 0) {
+      const unsigned long long t1 = x3_stamp();
+      tr[i] += t1 - tr_t0;
+      tr_t0 = t1;
+    }
+  };
   const int tid = threadIdx.x;
   const int lane = tid & 63;
-  const int wave = tid >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (scalar branches)
   const int li = lane & 31;
   const int lh = lane >> 5;
   const int b = blockIdx.z;
@@ -265,11 +338,35 @@ __global__ __launch_bounds__(NWV * 64) void conv_x3_kernel(const X3Args a) {
     *reinterpret_cast<h8*>(pl) = lo;
   };
 
+  // WL: chunk ch_ of class cls_ -> LDS [k-step][N-tile][hi|lo][lane], one 1-KB piece per
+  // wave-instruction (the LDS destination is the wave-uniform base + 16 B x lane)
+  // piece p = (k-step q, N-tile n, plane pl) of the chunk whose fragments start at src (+ lane)
+  auto w_piece = [&](int p, const uint4* src, _Float16* wdst) {
+    if constexpr (WL != 0) {
+      const int q = p / (WN * kNPL), r = p - q * (WN * kNPL);
+      const int n = r / kNPL, pl = r - n * kNPL;
+      const uint4* g = src + ((size_t)q * a.ntp + nt0 + n) * kFrag + pl * 64;
+      glds16(g, lds_addr(wdst + p * 512));
+    }
+  };
+  auto w_src = [&](int cls_, int ch_) {
+    return a.w + a.wcls[cls_] + (size_t)ch_ * a.nks[cls_] * a.ntp * kFrag + lane;
+  };
+  auto stage_w = [&](int cls_, int ch_, _Float16* wdst) {
+    if constexpr (WL != 0) {
+      const int np = a.nks[cls_] * WN * kNPL;
+      const uint4* src = w_src(cls_, ch_);
+      for (int p = wave; p < np; p += NWV) w_piece(p, src, wdst);
+    }
+  };
+
   for (int e = tid; e < tile_items; e += NT) {
     Stage st;
     fetch(e, w_first / a.nclass, 0, st);
     store(tile0, st);
   }
+  stage_w(cls, 0, wbase);
+  if constexpr (WL != 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (tid < WG * WN * 32) {
     const int j = nt0 * 32 + tid;
     sbias[tid] = j < a.cout ? a.bias[j] : 0.f;
@@ -285,12 +382,13 @@ __global__ __launch_bounds__(NWV * 64) void conv_x3_kernel(const X3Args a) {
   // without a memory wait inside the k-loop
   int tap_tab = a.toff[cls][lane <= kMaxTapsX ? lane : kMaxTapsX];
   __syncthreads();
+  TR(0);
 
   struct Ops {
     h8 ah[WM], al[WM];
-    uint4 bh[WN], bl[WN];
+    uint4 bh[WN], bl[WN], bm[kAcc1 ? WN : 1];
   };
-  f32x16 acc[WM][WN], cor[WM][WN];
+  f32x16 acc[WM][WN], cor[kAcc1 ? 1 : WM][kAcc1 ? 1 : WN];
   uint4 ko_w = a.w[lane];
   h8 ko_a = *reinterpret_cast<const h8*>(tile0 + 8 * lane);
   int buf = 0;  // LDS buffer holding the chunk being multiplied
@@ -317,7 +415,7 @@ __global__ __launch_bounds__(NWV * 64) void conv_x3_kernel(const X3Args a) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           acc[m][n][r] = 0.f;
-          cor[m][n][r] = 0.f;
+          if constexpr (!kAcc1) cor[m][n][r] = 0.f;
         }
 
     // K loop over channel chunks. Two operand register sets (ping-pong, no copies). Each
@@ -329,12 +427,28 @@ __global__ __launch_bounds__(NWV * 64) void conv_x3_kernel(const X3Args a) {
     for (int ch = 0; ch < nch; ++ch) {
       const _Float16* cur = tile0 + buf * tile_h;
       _Float16* nxt = tile0 + (buf ^ 1) * tile_h;
+      const uint4* wcur = reinterpret_cast<const uint4*>(wbase + buf * a.wl_h);
       const bool last = ch + 1 == nch;
       const int s_item = last ? squeue[(k + 1) & 3] : w;
       const int s_tile = s_item / a.nclass;
       const int s_ch = last ? 0 : ch + 1;
       const bool stage_next = s_item < nitems;
       const uint4* wch = wcls + (size_t)ch * nq * a.ntp * kFrag;
+      // WL: this wave's pieces of the next chunk's weights (issued after the chunk's first operand
+      // reads, landed by the vmcnt(0) before the chunk's closing barrier)
+      const int s_cls = s_item % a.nclass;
+      const uint4* wsrc = WL ? w_src(stage_next ? s_cls : 0, s_ch) : nullptr;
+      _Float16* const wdst = wbase + (buf ^ 1) * a.wl_h;
+      const int wnp = (WL && stage_next) ? a.nks[s_cls] * WN * kNPL : 0;
+      int wp = wave;
+      auto w_issue = [&]() {
+        if constexpr (WL != 0) {
+          if (wp < wnp) {
+            w_piece(wp, wsrc, wdst);
+            wp += NWV;
+          }
+        }
+      };
       // k-step q: lane half lh takes k8-block kb = 2q + lh = (tap kb / C8, octet kb % C8)
       auto load = [&](int q, Ops& op) {
         int toff;
@@ -355,7 +469,8 @@ __global__ __launch_bounds__(NWV * 64) void conv_x3_kernel(const X3Args a) {
           op.ah[m] = *reinterpret_cast<const h8*>(cur + pix0 + m * pix_m + toff);
           op.al[m] = *reinterpret_cast<const h8*>(cur + pix0 + m * pix_m + toff + C8 * a.ps);
         }
-        const uint4* wk = ((kKO & 16) ? wcls : wch) + ((size_t)((kKO & 16) ? 0 : q) * a.ntp + ntw) * kFrag + lane;
+        const uint4* wk = WL ? wcur + (size_t)q * WN * kFrag + lane
+                             : ((kKO & 16) ? wcls : wch) + ((size_t)((kKO & 16) ? 0 : q) * a.ntp + ntw) * kFrag + lane;
 #pragma unroll
         for (int n = 0; n < WN; ++n) {
           if constexpr ((kKO & 1) != 0) {
@@ -365,6 +480,7 @@ __global__ __launch_bounds__(NWV * 64) void conv_x3_kernel(const X3Args a) {
           }
           op.bh[n] = wk[n * kFrag];
           op.bl[n] = wk[n * kFrag + 64];
+          if constexpr (kAcc1) op.bm[n] = wk[n * kFrag + 128];
         }
       };
       // weights as the A (row) operand, pixels as B: the 32x32 result is channel x pixel, so
@@ -384,20 +500,44 @@ __global__ __launch_bounds__(NWV * 64) void conv_x3_kernel(const X3Args a) {
           for (int n = 0; n < WN; ++n) {
             const h8 wh = __builtin_bit_cast(h8, op.bh[n]);
             const h8 wl = __builtin_bit_cast(h8, op.bl[n]);
-            acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wh, op.ah[m], acc[m][n], 0, 0, 0);
-            cor[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wl, op.ah[m], cor[m][n], 0, 0, 0);
-            cor[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wh, op.al[m], cor[m][n], 0, 0, 0);
+            if constexpr (kAcc1) {
+              const h8 wm = __builtin_bit_cast(h8, op.bm[n]);
+              acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wh, op.ah[m], acc[m][n], 0, 0, 0);
+              acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wl, op.ah[m], acc[m][n], 0, 0, 0);
+              acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wm, op.al[m], acc[m][n], 0, 0, 0);
+            } else {
+              acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wh, op.ah[m], acc[m][n], 0, 0, 0);
+              cor[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wl, op.ah[m], cor[m][n], 0, 0, 0);
+              cor[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wh, op.al[m], cor[m][n], 0, 0, 0);
+            }
           }
+      };
+      // order pins inside a half-step (kSched 0) and the interleave pattern closing it (kSched 2)
+      auto pin = [&]() {
+        if constexpr (kSched == 0) __builtin_amdgcn_sched_barrier(0);
+      };
+      auto close = [&]() {
+        if constexpr (kSched == 2) {
+#pragma unroll
+          for (int i = 0; i < 3 * WM * WN; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // one MFMA
+            __builtin_amdgcn_sched_group_barrier(0x120, 1, 0);  // then one DS or VMEM read
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
       };
       auto half_plain = [&](int q, const Ops& use, Ops& nxt_ops) {
         load(q + 1 < nq ? q + 1 : nq - 1, nxt_ops);
-        __builtin_amdgcn_sched_barrier(0);
+        pin();
+        TR(1);
         mfmas(use);
-        __builtin_amdgcn_sched_barrier(0);
+        close();
+        TR(2);
       };
       int staged = 0;
       Ops S0, S1;
       load(0, S0);
+      while (wp < wnp) w_issue();  // WL: the next chunk's weights, a whole chunk ahead
       // staging items of the next chunk are spread evenly over the k-step pairs (one per staged
       // pair) so their VALU work interleaves with MFMA-only steps instead of bunching up at the
       // chunk start, where every wave would be VALU-bound at once
@@ -411,14 +551,19 @@ __global__ __launch_bounds__(NWV * 64) void conv_x3_kernel(const X3Args a) {
         load(q + 1 < nq ? q + 1 : nq - 1, S1);
         Stage st;
         fetch(stid + staged * NTS, s_tile, s_ch, st);
-        __builtin_amdgcn_sched_barrier(0);
+        pin();
+        TR(1);
         mfmas(S0);
-        __builtin_amdgcn_sched_barrier(0);
+        close();
+        TR(2);
         load(q + 2 < nq ? q + 2 : nq - 1, S0);
-        __builtin_amdgcn_sched_barrier(0);
+        pin();
+        TR(1);
         mfmas(S1);
-        __builtin_amdgcn_sched_barrier(0);
+        close();
+        TR(2);
         store(nxt, st);
+        TR(3);
         q += 2;
         for (int r = 1; r < spread; ++r, q += 2) {
           half_plain(q, S0, S1);
@@ -430,6 +575,7 @@ __global__ __launch_bounds__(NWV * 64) void conv_x3_kernel(const X3Args a) {
         half_plain(q + 1, S1, S0);
       }
       if (nq & 1) mfmas(S0);
+      TR(2);
       if (stage_next) {
         for (int qs = staged; qs < nstage; ++qs) {
           Stage st;
@@ -438,8 +584,10 @@ __global__ __launch_bounds__(NWV * 64) void conv_x3_kernel(const X3Args a) {
         }
       }
       if (ch == 0 && tid == 0) squeue[(k + 2) & 3] = taken;
+      if constexpr (WL != 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's weight DMA
       __syncthreads();
       buf ^= 1;
+      TR(4);
     }
 
     // epilogue of this tile (its global stores drain while the next tile's k-loop runs).
@@ -487,7 +635,8 @@ __global__ __launch_bounds__(NWV * 64) void conv_x3_kernel(const X3Args a) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int r = 4 * g + i;
-          const float tv = fmaf(cor[m][n][r], a.osc_c, fmaf(acc[m][n][r], a.osc, bb[i]));
+          const float tv = kAcc1 ? fmaf(acc[m][n][r], a.osc, bb[i])
+                                 : fmaf(cor[kAcc1 ? 0 : m][kAcc1 ? 0 : n][r], a.osc_c, fmaf(acc[m][n][r], a.osc, bb[i]));
           v[i] = fmaxf(tv, tv * a.act_slope);
         }
         if (a.res) {
@@ -503,14 +652,31 @@ __global__ __launch_bounds__(NWV * 64) void conv_x3_kernel(const X3Args a) {
                                                ry, so, 0, 0);
       }
     }
+    TR(5);
   }
   if (!(mx < 65000.f) && a.ovf) atomicOr(a.ovf, 1);
+#if FVC_X3_TRACE
+  {
+    const unsigned long long tr_end = x3_stamp();
+    tr[6] = tr_end - tr_begin;
+    tr[7] = 1;
+    const unsigned slot = ((blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) * NWV + wave;
+    if (lane < kTraceVals && slot < (unsigned)kTraceSlots) {
+      unsigned long long v = tr[0];
+#pragma unroll
+      for (int i = 1; i < kTraceVals; ++i) v = lane == i ? tr[i] : v;
+      atomicAdd(&g_x3_trace[(size_t)slot * kTraceVals + lane], v);
+    }
+  }
+#endif
   finish();
 }
 
 // ------------------------------------------------------------------ host-side geometry
 struct X3Cfg {
   int cinp, coutp, ntp, cc, wm, wn, nw, nclass, nchunks, th, sin, sout;
+  int wl;     // weights staged in LDS by LDS-DMA (FVC_X3_WL; chosen at pack time: it can shrink cc)
+  int wnmax;  // N-tiles per block the LDS weight buffers are sized for
   int ntaps[4], nks[4], oy0[4], ox0[4];
   int tky[4][kMaxTapsX], tkx[4][kMaxTapsX];
   int tdy[4][kMaxTapsX], tdx[4][kMaxTapsX];
@@ -604,12 +770,23 @@ static bool x3_cfg(int cin, int cout, int ks, int stride, int transposed, X3Cfg&
   // stride-2 convs: one strip per wave (measured 0.22 vs 0.35 ms on the 544x960 128-channel layer:
   // two strips double the halo rows each staged chunk carries)
   c.wm = env_int("FVC_X3_WM", (!transposed && stride == 2) ? 1 : 2) == 1 ? 1 : 2;
+  // weight buffers in LDS (WL): two chunks of the block's fragments, sized for its widest N
+  c.wl = env_int("FVC_X3_WL", 0) ? 1 : 0;
+  c.wnmax = (c.wm == 1 && !transposed && stride == 2 && c.ntp % 4 == 0) ? 4 : (c.ntp >= 2 ? 2 : 1);
   // shrink the channel chunk, then the strips per wave, until two tile buffers fit in LDS
   for (;;) {
     c.th = c.nw * c.wm;
     const int ir = (c.th - 1) * c.sin + 1 + (c.dymax - c.dymin);
     const int ic = 31 * c.sin + 1 + (c.dxmax - c.dxmin);
-    const size_t lds = 1024 + 2 * x3_tile_bytes(ir, ic, c.cc);
+    size_t lds = 1024 + 2 * x3_tile_bytes(ir, ic, c.cc);
+    if (c.wl) {
+      int nkmax = 0;
+      for (int cl = 0; cl < c.nclass; ++cl) {
+        const int nk = fvc_cdiv(c.ntaps[cl] * (c.cc / 8), 2);
+        nkmax = nk > nkmax ? nk : nkmax;
+      }
+      lds += 2 * (size_t)nkmax * c.wnmax * kFrag * 16;
+    }
     if (lds <= 160 * 1024) break;
     if (c.cc > 8 && c.cinp % (c.cc / 2) == 0) c.cc /= 2;
     else if (c.wm > 1) c.wm /= 2;
@@ -648,43 +825,43 @@ static int x3_kw(const float* w, size_t n) {
   return kw < -100 ? -100 : (kw > 100 ? 100 : kw);
 }
 
-template <int CC, int WM, int WN, int WG, int IOP, int POST, int NWV>
+template <int CC, int WM, int WN, int WG, int IOP, int POST, int NWV, int WL>
 static int x3_launch(const X3Args& a, dim3 grid, size_t lds, hipStream_t s) {
   if (lds > 64 * 1024)
-    (void)hipFuncSetAttribute((const void*)conv_x3_kernel<CC, WM, WN, WG, IOP, POST, NWV>,
+    (void)hipFuncSetAttribute((const void*)conv_x3_kernel<CC, WM, WN, WG, IOP, POST, NWV, WL>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL((conv_x3_kernel<CC, WM, WN, WG, IOP, POST, NWV>), grid, dim3(NWV * 64), lds, s, a);
+  hipLaunchKernelGGL((conv_x3_kernel<CC, WM, WN, WG, IOP, POST, NWV, WL>), grid, dim3(NWV * 64), lds, s, a);
   FVC_CHECK_LAUNCH();
   return 0;
 }
 
 // exp after the epilogue is only ever taken with an untransformed input (Synthesis_prior_net
 // deconv3, synthesis_prior.py:25,57): instantiated for IN_NONE only
-template <int CC, int WM, int WN, int WG, int NWV = 8>
+template <int CC, int WM, int WN, int WG, int WL, int NWV = 8>
 static int x3_launch_iop(int iop, int post, const X3Args& a, dim3 grid, size_t lds, hipStream_t s) {
   if (post == FVC_POST_EXP)
-    return iop == FVC_IN_NONE ? x3_launch<CC, WM, WN, WG, FVC_IN_NONE, FVC_POST_EXP, NWV>(a, grid, lds, s) : FVC_EINVAL;
+    return iop == FVC_IN_NONE ? x3_launch<CC, WM, WN, WG, FVC_IN_NONE, FVC_POST_EXP, NWV, WL>(a, grid, lds, s) : FVC_EINVAL;
   switch (iop) {
-    case FVC_IN_NONE: return x3_launch<CC, WM, WN, WG, FVC_IN_NONE, FVC_POST_NONE, NWV>(a, grid, lds, s);
-    case FVC_IN_RELU: return x3_launch<CC, WM, WN, WG, FVC_IN_RELU, FVC_POST_NONE, NWV>(a, grid, lds, s);
-    case FVC_IN_ABS: return x3_launch<CC, WM, WN, WG, FVC_IN_ABS, FVC_POST_NONE, NWV>(a, grid, lds, s);
-    case FVC_IN_ROUND: return x3_launch<CC, WM, WN, WG, FVC_IN_ROUND, FVC_POST_NONE, NWV>(a, grid, lds, s);
+    case FVC_IN_NONE: return x3_launch<CC, WM, WN, WG, FVC_IN_NONE, FVC_POST_NONE, NWV, WL>(a, grid, lds, s);
+    case FVC_IN_RELU: return x3_launch<CC, WM, WN, WG, FVC_IN_RELU, FVC_POST_NONE, NWV, WL>(a, grid, lds, s);
+    case FVC_IN_ABS: return x3_launch<CC, WM, WN, WG, FVC_IN_ABS, FVC_POST_NONE, NWV, WL>(a, grid, lds, s);
+    case FVC_IN_ROUND: return x3_launch<CC, WM, WN, WG, FVC_IN_ROUND, FVC_POST_NONE, NWV, WL>(a, grid, lds, s);
   }
   return FVC_EINVAL;
 }
 
 // instantiated wave grids (8 waves, 2 per SIMD, <= 256 registers: scripts/kres.sh):
 // WG = 1 with WM, WN in {1, 2} or WM = 1, WN = 4; WG = 2 with WM = 4, WN = 1
-template <int CC>
+template <int CC, int WL>
 static int x3_launch_cc(int nwv, int wm, int wn, int wg, int iop, int post, const X3Args& a, dim3 grid,
                         size_t lds, hipStream_t s) {
   if (nwv != 8) return FVC_EINVAL;
-  if (wg == 2) return (wm == 4 && wn == 1) ? x3_launch_iop<CC, 4, 1, 2>(iop, post, a, grid, lds, s) : FVC_EINVAL;
-  if (wm == 2 && wn == 2) return x3_launch_iop<CC, 2, 2, 1>(iop, post, a, grid, lds, s);
-  if (wm == 2 && wn == 1) return x3_launch_iop<CC, 2, 1, 1>(iop, post, a, grid, lds, s);
-  if (wm == 1 && wn == 2) return x3_launch_iop<CC, 1, 2, 1>(iop, post, a, grid, lds, s);
-  if (wm == 1 && wn == 1) return x3_launch_iop<CC, 1, 1, 1>(iop, post, a, grid, lds, s);
-  if (wm == 1 && wn == 4) return x3_launch_iop<CC, 1, 4, 1>(iop, post, a, grid, lds, s);
+  if (wg == 2) return (wm == 4 && wn == 1 && !WL) ? x3_launch_iop<CC, 4, 1, 2, 0>(iop, post, a, grid, lds, s) : FVC_EINVAL;
+  if (wm == 2 && wn == 2) return x3_launch_iop<CC, 2, 2, 1, WL>(iop, post, a, grid, lds, s);
+  if (wm == 2 && wn == 1) return x3_launch_iop<CC, 2, 1, 1, WL>(iop, post, a, grid, lds, s);
+  if (wm == 1 && wn == 2) return x3_launch_iop<CC, 1, 2, 1, WL>(iop, post, a, grid, lds, s);
+  if (wm == 1 && wn == 1) return x3_launch_iop<CC, 1, 1, 1, WL>(iop, post, a, grid, lds, s);
+  if (wm == 1 && wn == 4) return x3_launch_iop<CC, 1, 4, 1, WL>(iop, post, a, grid, lds, s);
   return FVC_EINVAL;
 }
 
@@ -762,7 +939,6 @@ static int run_x3(const float* x, const void* wpack, float osc, const float* bia
       a.toff[cl][t] = off;
     }
   size_t lds = 1024 + 2 * x3_tile_bytes(a.ir, a.ic, c.cc);
-  if (lds > 160 * 1024) return FVC_EINVAL;
   const int tiles_x = fvc_cdiv(a.Wq, 32);
   const int tiles_y = fvc_cdiv(a.Hq, th);
   // N-tiles per block: 2 (each staged input element feeds 64 output channels) unless the layer
@@ -779,12 +955,21 @@ static int run_x3(const float* x, const void* wpack, float osc, const float* bia
   // two N-groups of 4 waves x 4 strips instead of 8 waves x 2 strips x 2 N-tiles (same block
   // tile: 16 rows x 32 pixels x 64 channels): each weight fragment feeds 4 strips
   int wm = c.wm, wg = 1;
-  if (c.nw == 8 && env_int("FVC_X3_WG", 0) == 2 && c.wm == 2 && wn == 2) {
+  if (c.nw == 8 && !c.wl && env_int("FVC_X3_WG", 0) == 2 && c.wm == 2 && wn == 2) {
     wm = 4;
     wn = 1;
     wg = 2;
   }
   const int nb = wn * wg;  // N-tiles per block
+  if (wn > c.wnmax && c.wl) return FVC_EINVAL;
+  a.wl_h = 0;
+  if (c.wl) {
+    int nkmax = 0;
+    for (int cl = 0; cl < c.nclass; ++cl) nkmax = c.nks[cl] > nkmax ? c.nks[cl] : nkmax;
+    a.wl_h = nkmax * wn * kFrag * 8;  // halves
+    lds += 2 * (size_t)a.wl_h * 2;
+  }
+  if (lds > 160 * 1024) return FVC_EINVAL;
   // persistent grid: ~one 8-wave block per CU (FVC_X3_BPC blocks per CU), each walking a
   // contiguous run of spatial tiles
   // cu_reserve CUs are left out of the persistent grid for kernels of other streams (the
@@ -800,10 +985,18 @@ static int run_x3(const float* x, const void* wpack, float osc, const float* bia
   dim3 grid((unsigned)gx, c.ntp / nb, batch);
   // dynamic schedule when the caller's scratch holds the group counters (FVC_X3_DYN=0: static runs)
   a.sched = (sched && sched_len >= 1 + (long long)grid.y * grid.z && env_int("FVC_X3_DYN", 1)) ? sched : nullptr;
+  if (c.wl) {
+    switch (c.cc) {
+      case 8: return x3_launch_cc<8, 1>(c.nw, wm, wn, wg, in_op, post_op, a, grid, lds, s);
+      case 16: return x3_launch_cc<16, 1>(c.nw, wm, wn, wg, in_op, post_op, a, grid, lds, s);
+      case 32: return x3_launch_cc<32, 1>(c.nw, wm, wn, wg, in_op, post_op, a, grid, lds, s);
+    }
+    return FVC_EINVAL;
+  }
   switch (c.cc) {
-    case 8: return x3_launch_cc<8>(c.nw, wm, wn, wg, in_op, post_op, a, grid, lds, s);
-    case 16: return x3_launch_cc<16>(c.nw, wm, wn, wg, in_op, post_op, a, grid, lds, s);
-    case 32: return x3_launch_cc<32>(c.nw, wm, wn, wg, in_op, post_op, a, grid, lds, s);
+    case 8: return x3_launch_cc<8, 0>(c.nw, wm, wn, wg, in_op, post_op, a, grid, lds, s);
+    case 16: return x3_launch_cc<16, 0>(c.nw, wm, wn, wg, in_op, post_op, a, grid, lds, s);
+    case 32: return x3_launch_cc<32, 0>(c.nw, wm, wn, wg, in_op, post_op, a, grid, lds, s);
   }
   return FVC_EINVAL;
 }
@@ -811,6 +1004,18 @@ static int run_x3(const float* x, const void* wpack, float osc, const float* bia
 }  // namespace
 
 extern "C" {
+
+#if FVC_X3_TRACE
+// diagnostic builds: copy (and clear) the per-wave segment sums [slot][8]
+int fvc_x3_trace_read(unsigned long long* host, int nslots) {
+  if (nslots > kTraceSlots) nslots = kTraceSlots;
+  if (hipDeviceSynchronize() != hipSuccess) return FVC_EINVAL;
+  if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_x3_trace), (size_t)nslots * kTraceVals * 8) != hipSuccess) return FVC_EINVAL;
+  static unsigned long long zeros[kTraceSlots * kTraceVals];
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_x3_trace), zeros, sizeof(zeros)) != hipSuccess) return FVC_EINVAL;
+  return 0;
+}
+#endif
 
 int fvc_conv_x3_supported(int cin, int cout, int ksize, int stride, int transposed) {
   X3Cfg c;
@@ -853,7 +1058,12 @@ int fvc_conv_x3_pack_weight(const float* w, void* wp, float* osc_out, int cin, i
                                           : w[(((size_t)j * cin + ci) * ks + ky) * ks + kx]) * sc;
               const _Float16 hi = (_Float16)v;
               out[frag + e] = hi;  // plane 0 (hi): lanes 0..63
-              out[frag + 64 * 8 + e] = (_Float16)((v - (float)hi) * 2048.f);   // plane 1: lo * 2^11
+              if (kAcc1) {
+                out[frag + 64 * 8 + e] = (_Float16)(v - (float)hi);                 // plane 1: w - hi
+                out[frag + 128 * 8 + e] = (_Float16)((float)hi * (1.f / 2048.f));  // plane 2: hi 2^-11
+              } else {
+                out[frag + 64 * 8 + e] = (_Float16)((v - (float)hi) * 2048.f);  // plane 1: lo * 2^11
+              }
             }
           }
   return 0;
