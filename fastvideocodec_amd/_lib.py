@@ -29,6 +29,13 @@ _SIGS = {
     "fvc_conv_x3_pack_weight": (c_int, [vp, vp, vp] + [c_int] * 5),
     "fvc_conv2d_nhwc_x3": (c_int, [vp, vp, c_float, vp, vp, vp] + [c_int] * 11 + [vp, vp, c_int, vp]),
     "fvc_deconv2d_nhwc_x3": (c_int, [vp, vp, c_float, vp, vp, vp] + [c_int] * 11 + [vp, vp, c_int, vp]),
+    "fvc_conv_x3_tap_supported": (c_int, [c_int] * 6),
+    "fvc_x3_tap_wpack_bytes": (c_size_t, [c_int, c_int]),
+    "fvc_x3_tap_pack_weight": (c_int, [vp, vp, vp, c_int, c_int]),
+    "fvc_conv2d_nhwc_x3_tap": (c_int, [vp, vp, c_float, vp, vp, vp] + [c_int] * 8 + [vp, c_float]
+                               + [c_int] * 2 + [vp, vp, c_int, vp]),
+    "fvc_deconv2d_nhwc_x3_tap": (c_int, [vp, vp, c_float, vp, vp, vp] + [c_int] * 8 + [vp, c_float]
+                                 + [c_int] * 2 + [vp, vp, c_int, vp]),
     "fvc_nchw_to_nhwc": (c_int, [vp, vp, c_int, c_int, c_int, c_int, c_int, vp]),
     "fvc_nhwc_to_nchw": (c_int, [vp, vp, c_int, c_int, c_int, c_int, c_int, c_int, vp]),
     "fvc_avgpool2_nhwc": (c_int, [vp, vp, c_int, c_int, c_int, c_int, vp]),

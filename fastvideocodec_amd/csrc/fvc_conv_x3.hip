@@ -81,6 +81,8 @@ constexpr int kSched = FVC_X3_SCHED;
 constexpr int kAcc1 = FVC_X3_ACC1;
 constexpr int kNPL = kAcc1 ? 3 : 2;        // weight planes per (k-step, N-tile): hi, lo [, hi 2^-11]
 constexpr int kFrag = 64 * kNPL;          // uint4 per (k-step, N-tile)
+// internal post-op of the fused tap path (fvc_conv2d_nhwc_x3_tap): not part of the public enum
+constexpr int kPostTap = 2;
 
 struct X3Args {
   const float* x;
@@ -111,6 +113,12 @@ struct X3Args {
   int prio;                        // static priority 1 for the second-dispatched half (waves 4-7)
   int* ovf;                        // caller's overflow flag (device int; may be null)
   int wl_h;                        // WL: halves per LDS weight buffer (the chunk's fragments)
+  unsigned res_bytes;              // bytes of res (its own descriptor range)
+  // POST == kPostTap: the epilogue applies the next layer's 1x1 tap-partial GEMM to the finished
+  // output tile and writes P [B][Ho][Wo][pcp] to y instead of the tile itself
+  const uint4* tw;                 // tap weights [k16 block][hi|lo][lane] (fvc_x3_tap_pack_weight)
+  float tosc, tosc_c;              // 2^-kt, 2^-kt-11
+  int pcp;                         // P channels (partials rounded up to 4, <= 32)
   int toff[4][kMaxTapsX + 1];      // LDS offset (halves) of each tap's window; 0 past ntaps
 };
 
@@ -395,7 +403,7 @@ __global__ __launch_bounds__(NWV * 64) void conv_x3_kernel(const X3Args a) {
   const __amdgpu_buffer_rsrc_t ry =
       __builtin_amdgcn_make_buffer_rsrc((void*)a.y, (short)0, (int)a.y_bytes, kRsrcFlags);
   const __amdgpu_buffer_rsrc_t rr =
-      __builtin_amdgcn_make_buffer_rsrc((void*)a.res, (short)0, (int)a.y_bytes, kRsrcFlags);
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.res, (short)0, (int)a.res_bytes, kRsrcFlags);
   for (int k = 0;; ++k) {
     const int w = squeue[k & 3];
     if (w >= nitems) break;
@@ -598,11 +606,77 @@ __global__ __launch_bounds__(NWV * 64) void conv_x3_kernel(const X3Args a) {
     // channels are 0, so they come out 0 -- except after exp (POST), which selects them to 0.
     const int qy0 = (tile / tiles_x) * TH, qx0 = (tile % tiles_x) * TW;
     const bool px_ok = qx0 + li < a.Wq;
-    auto voff_of = [&](int m, int n) {
+    auto pix_of = [&](int m) {  // output pixel index of this lane in strip m
       const unsigned qy = qy0 + wm_ * WM + m;
-      return (((unsigned)b * a.Ho + qy * a.sout + a.oy0[cls]) * a.Wo + a.ox0[cls] +
-              (unsigned)(qx0 + li) * a.sout) * (unsigned)a.coutp * 4u + (unsigned)((ntw + n) * 32 + 4 * lh) * 4u;
+      return ((unsigned)b * a.Ho + qy * a.sout + a.oy0[cls]) * a.Wo + a.ox0[cls] + (unsigned)(qx0 + li) * a.sout;
     };
+    auto voff_of = [&](int m, int n) {
+      return pix_of(m) * (unsigned)a.coutp * 4u + (unsigned)((ntw + n) * 32 + 4 * lh) * 4u;
+    };
+    if constexpr (POST == kPostTap) {
+      // Fused tap-partial epilogue (the next layer is a cout <= 4 conv computed as a 1x1 GEMM to
+      // P = k*k*cout tap partials per pixel + fvc_tap_gather_nhwc). This wave holds every output
+      // channel of its strips (WG = 1, WN = all N-tiles): lane (li, lh) has channel
+      // 32n + 8g + 4lh + i of pixel li in register 4g + i of tile (m, n), so registers 8gp..8gp+7
+      // of tile n are exactly the B operand of the k16 block kb = 2n + gp (channels
+      // 32n + 16gp + {0-3, 8-11 | 4-7, 12-15} for lane half 0 | 1; the tap pack uses the same order).
+      // The finished values y are split hi/lo like staged activations and multiplied with the
+      // same three MFMAs per block; P = main * 2^-kt + corr * 2^-kt-11.
+#pragma unroll
+      for (int m = 0; m < WM; ++m) {
+        const unsigned pix = pix_of(m);
+        const bool row_ok = qy0 + wm_ * WM + m < a.Hq && px_ok;
+        f32x16 pa, pc;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) pa[r] = pc[r] = 0.f;
+        // tile by tile: finish y of N-tile n (bias, act, residual), then its two k16 blocks, so
+        // only one tile's y is live next to the partial accumulators
+#pragma unroll
+        for (int n = 0; n < WN; ++n) {
+          float yv[16];
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            float4 rq = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (a.res) rq = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rr, voff_of(m, n) + 32u * g, 0, 0));
+            const float4 bj = *reinterpret_cast<const float4*>(sbias + n * 32 + 8 * g + 4 * lh);
+            const float bb[4] = {bj.x, bj.y, bj.z, bj.w};
+            const float rr4[4] = {rq.x, rq.y, rq.z, rq.w};
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const int r = 4 * g + i;
+              const float tv = fmaf(cor[kAcc1 ? 0 : m][kAcc1 ? 0 : n][r], kAcc1 ? 0.f : a.osc_c, fmaf(acc[m][n][r], a.osc, bb[i]));
+              yv[r] = fmaxf(tv, tv * a.act_slope) + rr4[i];
+            }
+          }
+#pragma unroll
+          for (int gp = 0; gp < 2; ++gp) {
+            float v8[8];
+#pragma unroll
+            for (int t = 0; t < 8; ++t) v8[t] = yv[8 * gp + t];
+            h8 yh, yl;
+            split8(v8, yh, yl, mx);
+            const uint4* tw = a.tw + (size_t)((n * 2 + gp) * 2) * 64 + lane;
+            const h8 wh = __builtin_bit_cast(h8, tw[0]);
+            const h8 wl = __builtin_bit_cast(h8, tw[64]);
+            pa = __builtin_amdgcn_mfma_f32_32x32x16_f16(wh, yh, pa, 0, 0, 0);
+            pc = __builtin_amdgcn_mfma_f32_32x32x16_f16(wl, yh, pc, 0, 0, 0);
+            pc = __builtin_amdgcn_mfma_f32_32x32x16_f16(wh, yl, pc, 0, 0, 0);
+          }
+        }
+        const unsigned po = pix * (unsigned)a.pcp * 4u + (unsigned)(4 * lh) * 4u;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int p0 = 8 * g + 4 * lh;
+          float o[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) o[i] = fmaf(pc[4 * g + i], a.tosc_c, pa[4 * g + i] * a.tosc);
+          const unsigned so = (row_ok && p0 < a.pcp) ? po + 32u * g : kOob;
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, make_float4(o[0], o[1], o[2], o[3])), ry, so, 0, 0);
+        }
+      }
+      TR(5);
+      continue;
+    }
     // residual: the 4 groups of output tile t+1 are loaded before tile t is finished and stored,
     // so each wait covers loads issued one tile earlier (vmcnt is in order and counts the stores);
     // WM = WN = 2 has no registers for the second set: its 4 loads are waited for together
@@ -839,6 +913,11 @@ static int x3_launch(const X3Args& a, dim3 grid, size_t lds, hipStream_t s) {
 // deconv3, synthesis_prior.py:25,57): instantiated for IN_NONE only
 template <int CC, int WM, int WN, int WG, int WL, int NWV = 8>
 static int x3_launch_iop(int iop, int post, const X3Args& a, dim3 grid, size_t lds, hipStream_t s) {
+  if (post == kPostTap) {  // fused tap epilogue: every output channel in one wave (run_x3)
+    if constexpr (WG == 1 && WL == 0 && ((WM == 2 && WN <= 2) || (WM == 1 && WN == 4)))
+      return iop == FVC_IN_NONE ? x3_launch<CC, WM, WN, WG, FVC_IN_NONE, kPostTap, NWV, WL>(a, grid, lds, s) : FVC_EINVAL;
+    return FVC_EINVAL;
+  }
   if (post == FVC_POST_EXP)
     return iop == FVC_IN_NONE ? x3_launch<CC, WM, WN, WG, FVC_IN_NONE, FVC_POST_EXP, NWV, WL>(a, grid, lds, s) : FVC_EINVAL;
   switch (iop) {
@@ -865,15 +944,29 @@ static int x3_launch_cc(int nwv, int wm, int wn, int wg, int iop, int post, cons
   return FVC_EINVAL;
 }
 
+// tw != null: fused tap epilogue (y receives P [batch][Ho][Wo][pcp], see kPostTap)
 static int run_x3(const float* x, const void* wpack, float osc, const float* bias, const float* res,
                   float* y, int batch, int h, int w, int cin, int cout, int ks, int stride, int transposed,
                   int in_op, int act, int post_op, int cu_reserve, int* ovf, int* sched, int sched_len,
-                  hipStream_t s) {
+                  hipStream_t s, const void* tw = nullptr, float tosc = 0.f, int pcp = 0) {
   X3Cfg c;
   if (!x3_cfg(cin, cout, ks, stride, transposed, c)) return FVC_EINVAL;
   if (!x || !wpack || !bias || !y || batch <= 0 || h <= 0 || w <= 0) return FVC_EINVAL;
+  if (tw) {
+    // every output channel in one wave: N-tiles 1, 2 (2 strips per wave) or 4 (1 strip); the
+    // channel chunk (and so the weight pack) stays what x3_cfg chose: fewer strips only shrink LDS
+    if (post_op != FVC_POST_NONE || in_op != FVC_IN_NONE || c.wl || c.ntp == 3 || c.ntp > 4 || pcp <= 0 ||
+        pcp > 32 || (pcp & 3))
+      return FVC_EINVAL;
+    if (c.ntp == 4) c.wm = 1;
+    c.th = c.nw * c.wm;
+    post_op = kPostTap;
+  }
+  const int ych = tw ? pcp : c.coutp;  // channels of the tensor y points to
   X3Args a;
   a.x = x; a.w = (const uint4*)wpack; a.bias = bias; a.res = res; a.y = y;
+  a.tw = (const uint4*)tw; a.pcp = pcp;
+  a.tosc = tosc; a.tosc_c = tosc * (1.0f / 2048.f);
   a.B = batch; a.H = h; a.W = w; a.cinp = c.cinp;
   a.coutp = c.coutp; a.cout = cout;
   if (!transposed) {
@@ -886,20 +979,23 @@ static int run_x3(const float* x, const void* wpack, float osc, const float* bia
   }
   // y and res are addressed through buffer descriptors with 32-bit offsets: split batches whose
   // output tensor reaches 4 GB into launches over sub-batches
-  const unsigned long long ybytes = (unsigned long long)batch * a.Ho * a.Wo * a.coutp * 4ull;
+  const unsigned long long ybytes = (unsigned long long)batch * a.Ho * a.Wo * ych * 4ull;
+  const unsigned long long rbytes = (unsigned long long)batch * a.Ho * a.Wo * a.coutp * 4ull;
   const long long split_env = env_int("FVC_X3_SPLIT_BYTES", 0);  // tests: force the split path
   const unsigned long long split_at = split_env > 0 ? (unsigned long long)split_env : (1ull << 32) - 4096;
-  if (ybytes >= split_at) {
+  if (ybytes >= split_at || (res && rbytes >= split_at)) {
     if (batch == 1) return FVC_EINVAL;
     const int b1 = batch / 2;
-    const size_t xs = (size_t)h * w * c.cinp, ys = (size_t)a.Ho * a.Wo * a.coutp;
+    const size_t xs = (size_t)h * w * c.cinp, ys = (size_t)a.Ho * a.Wo * ych, rs = (size_t)a.Ho * a.Wo * c.coutp;
+    const int post_in = tw ? FVC_POST_NONE : post_op;
     int rc = run_x3(x, wpack, osc, bias, res, y, b1, h, w, cin, cout, ks, stride, transposed, in_op, act,
-                    post_op, cu_reserve, ovf, sched, sched_len, s);
+                    post_in, cu_reserve, ovf, sched, sched_len, s, tw, tosc, pcp);
     if (rc) return rc;
-    return run_x3(x + b1 * xs, wpack, osc, bias, res ? res + b1 * ys : nullptr, y + b1 * ys, batch - b1, h, w, cin, cout, ks,
-                  stride, transposed, in_op, act, post_op, cu_reserve, ovf, sched, sched_len, s);
+    return run_x3(x + b1 * xs, wpack, osc, bias, res ? res + b1 * rs : nullptr, y + b1 * ys, batch - b1, h, w, cin, cout, ks,
+                  stride, transposed, in_op, act, post_in, cu_reserve, ovf, sched, sched_len, s, tw, tosc, pcp);
   }
   a.y_bytes = (unsigned)ybytes;
+  a.res_bytes = (unsigned)rbytes;
   // the input is addressed per image (blockIdx.z) through a 32-bit-range descriptor too
   const unsigned long long xbytes = (unsigned long long)h * w * c.cinp * 4ull;
   if (xbytes >= (1ull << 32) - 4096) return FVC_EINVAL;
@@ -946,16 +1042,17 @@ static int run_x3(const float* x, const void* wpack, float osc, const float* bia
   // stride-2 convs (one strip per wave) with 4 N-tiles take all 128 channels per block: the
   // input tile is staged once instead of twice (3x3 s2 128->128 at 544x960: 0.214 -> 0.191 ms)
   int wn = (c.wm == 1 && !transposed && stride == 2 && c.ntp % 4 == 0) ? 4 : (c.ntp >= 2 ? 2 : 1);
-  const int want_wn = env_int("FVC_X3_WN", 0);
+  const int want_wn = tw ? c.ntp : env_int("FVC_X3_WN", 0);
   if (want_wn == 1 || want_wn == 2 || (want_wn == 4 && c.wm == 1)) wn = want_wn;
   while (wn > 1 && c.ntp % wn) wn >>= 1;
   const long long base = (long long)tiles_x * tiles_y * batch * c.nclass;
   if (!want_wn)
     while (wn > 1 && base * (c.ntp / wn) < 2LL * x3_num_cus()) wn >>= 1;
+  if (tw && wn != c.ntp) return FVC_EINVAL;
   // two N-groups of 4 waves x 4 strips instead of 8 waves x 2 strips x 2 N-tiles (same block
   // tile: 16 rows x 32 pixels x 64 channels): each weight fragment feeds 4 strips
   int wm = c.wm, wg = 1;
-  if (c.nw == 8 && !c.wl && env_int("FVC_X3_WG", 0) == 2 && c.wm == 2 && wn == 2) {
+  if (c.nw == 8 && !c.wl && !tw && env_int("FVC_X3_WG", 0) == 2 && c.wm == 2 && wn == 2) {
     wm = 4;
     wn = 1;
     wg = 2;
@@ -1067,6 +1164,67 @@ int fvc_conv_x3_pack_weight(const float* w, void* wp, float* osc_out, int cin, i
             }
           }
   return 0;
+}
+
+// tap weights for the fused epilogue: w [np][cin] (np = k*k*cout partials of the next layer,
+// row t*cout + co), cin = this conv's cout. Layout [k16 block kb][hi|lo][lane] of 16-B fragments;
+// lane (li, lh) of block kb holds row li, channels 16kb + 4lh + {0,1,2,3,8,9,10,11} (the
+// accumulator order of the producing tile, kPostTap), scaled by 2^kt like the conv packs.
+static int x3_tap_blocks(int cin) { return 2 * fvc_cdiv(fvc_rup(cin, 4), 32); }
+
+size_t fvc_x3_tap_wpack_bytes(int np, int cin) {
+  if (np <= 0 || np > 32 || cin <= 0 || cin > 128) return 0;
+  return (size_t)x3_tap_blocks(cin) * 2 * 64 * 16;
+}
+
+int fvc_x3_tap_pack_weight(const float* w, void* wp, float* osc_out, int np, int cin) {
+  if (!w || !wp || !osc_out || !fvc_x3_tap_wpack_bytes(np, cin)) return FVC_EINVAL;
+  const int kw = x3_kw(w, (size_t)np * cin);
+  const float sc = ldexpf(1.f, kw);
+  *osc_out = ldexpf(1.f, -kw);
+  _Float16* out = (_Float16*)wp;
+  const int nkb = x3_tap_blocks(cin);
+  for (int kb = 0; kb < nkb; ++kb)
+    for (int lane = 0; lane < 64; ++lane) {
+      const int li = lane & 31, lh = lane >> 5;
+      for (int t = 0; t < 8; ++t) {
+        const int ci = 16 * kb + (t < 4 ? t : t + 4) + 4 * lh;
+        const float v = (li < np && ci < cin) ? w[(size_t)li * cin + ci] * sc : 0.f;
+        const _Float16 hi = (_Float16)v;
+        out[((size_t)(kb * 2 + 0) * 64 + lane) * 8 + t] = hi;
+        out[((size_t)(kb * 2 + 1) * 64 + lane) * 8 + t] = (_Float16)((v - (float)hi) * 2048.f);
+      }
+    }
+  return 0;
+}
+
+int fvc_conv_x3_tap_supported(int cin, int cout, int ksize, int stride, int transposed, int pcp) {
+  X3Cfg c;
+  if (!x3_cfg(cin, cout, ksize, stride, transposed, c) || c.wl || pcp <= 0 || pcp > 32 || (pcp & 3)) return 0;
+  const int wm = c.ntp == 4 ? 1 : c.wm;
+  return (wm == 2 && c.ntp <= 2) || (wm == 1 && c.ntp == 4);
+}
+
+int fvc_conv2d_nhwc_x3_tap(const float* x, const void* wpack, float osc, const float* bias, const float* res,
+                           float* P, int batch, int h, int w, int cin, int cout, int ksize, int stride, int act,
+                           const void* tap_wpack, float tap_osc, int pcp, int cu_reserve, int* overflow_flag,
+                           int* sched, int sched_len, fvc_stream_t stream) {
+  if (cu_reserve < 0 || sched_len < 0 || !tap_wpack || !fvc_conv_x3_tap_supported(cin, cout, ksize, stride, 0, pcp))
+    return FVC_EINVAL;
+  return run_x3(x, wpack, osc, bias, res, P, batch, h, w, cin, cout, ksize, stride, 0, FVC_IN_NONE, act,
+                FVC_POST_NONE, cu_reserve, overflow_flag, sched, sched_len, (hipStream_t)stream, tap_wpack, tap_osc,
+                pcp);
+}
+
+int fvc_deconv2d_nhwc_x3_tap(const float* x, const void* wpack, float osc, const float* bias, const float* res,
+                             float* P, int batch, int h, int w, int cin, int cout, int ksize, int stride, int act,
+                             const void* tap_wpack, float tap_osc, int pcp, int cu_reserve, int* overflow_flag,
+                             int* sched, int sched_len, fvc_stream_t stream) {
+  if (cu_reserve < 0 || sched_len < 0 || !tap_wpack || !fvc_conv_x3_tap_supported(cin, cout, ksize, stride, 1, pcp))
+    return FVC_EINVAL;
+  return run_x3(x, wpack, osc, bias, res, P, batch, h, w, cin, cout, ksize, stride, 1, FVC_IN_NONE, act,
+                FVC_POST_NONE, cu_reserve, overflow_flag, sched, sched_len, (hipStream_t)stream, tap_wpack, tap_osc,
+                pcp);
 }
 
 int fvc_conv2d_nhwc_x3(const float* x, const void* wpack, float osc, const float* bias,

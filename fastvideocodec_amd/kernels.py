@@ -332,6 +332,94 @@ class PackedConv:
         return y
 
 
+    def tap_fusable(self, tap: "TapConsumer") -> bool:
+        """True if this conv can run with ``tap``'s 1x1 partial GEMM fused into its epilogue
+        (split-precision path, its output feeds tap's layer, every output channel in one wave)."""
+        return (self.x3 and self.tap is None and cp4(self.cout) == cp4(tap.cin) and
+                bool(_lib.load().fvc_conv_x3_tap_supported(self.cin, self.cout, self.ksize, self.stride,
+                                                            int(self.transposed), tap.pcp)))
+
+    def call_tap(self, x, tap: "TapConsumer", act=ACT_NONE, res=None):
+        """This conv (in_op none, act, res) fused with the first half of ``tap``'s layer: returns
+        P [B, Ho, Wo, tap.pcp] = tap partials of the output (which itself is never written);
+        ``tap.gather(P, ...)`` finishes the next layer (fvc_conv2d_nhwc_x3_tap)."""
+        if not self.tap_fusable(tap):
+            raise ValueError("conv / tap pair not fusable")
+        B, H, W, cp = x.shape
+        if cp != cp4(self.cin):
+            raise ValueError(f"conv input has {cp} channels, expected {cp4(self.cin)}")
+        if (not self.transposed) and self.stride == 2 and (H % 2 or W % 2):
+            raise ValueError("stride-2 conv needs even input size")
+        _chk(x, name="x")
+        ho, wo = self.out_hw(H, W)
+        _chk(res, (B, ho, wo, cp4(self.cout)), name="res")
+        P = torch.empty((B, ho, wo, tap.pcp), dtype=torch.float32, device=x.device)
+        timer = profiling.active()
+        if timer is not None:
+            ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            ev0.record()
+        fn = "fvc_deconv2d_nhwc_x3_tap" if self.transposed else "fvc_conv2d_nhwc_x3_tap"
+        _lib.call(fn, x.data_ptr(), self.wpack.data_ptr(), self.osc, self.bias.data_ptr(), _ptr(res), P.data_ptr(),
+                  B, H, W, self.cin, self.cout, self.ksize, self.stride, act, tap.wpack.data_ptr(), tap.osc, tap.pcp,
+                  _STATE["cu_reserve"], overflow_flag(x.device).data_ptr(), sched_scratch(x.device).data_ptr(),
+                  SCHED_LEN, stream_handle())
+        if timer is not None:
+            ev1.record()
+            # algorithmic work: this conv + the next layer's MACs (the partial GEMM does all of them)
+            fl = (profiling.conv_flops(self.cin, self.cout, self.ksize, self.stride, self.transposed, B, H, W) +
+                  2.0 * B * ho * wo * tap.cin * tap.np)
+            nbytes = 4 * (x.numel() + P.numel() + (res.numel() if res is not None else 0)) + \
+                self.wpack.numel() * self.wpack.element_size() + tap.wpack.numel() * tap.wpack.element_size()
+            timer.records.append((ev0, ev1, fl, f"{'deconv' if self.transposed else 'conv'}{self.ksize}s{self.stride} "
+                                  f"{self.cin}->{self.cout} @{H}x{W} x3 +tap{tap.ksize}x{tap.ksize}->{tap.cout}",
+                                  True, nbytes))
+        return P
+
+
+class TapConsumer:
+    """A cout <= 4 conv (stride 1) / transposed conv (stride 2) in tap-partial form for fusion into
+    its producer's epilogue: np = k*k*cout partial rows [t*cout + co][cin] (t = ky*k + kx), packed
+    for the producer tile's accumulator order (fvc_x3_tap_pack_weight), plus the gather that sums
+    them into the layer's output (fvc_tap_gather_nhwc). Used for synthesis_mv.py:41-43
+    (deconv7 -> deconv8) and endecoder.py:278-279 (Warp_net conv5 -> conv6)."""
+
+    def __init__(self, weight: torch.Tensor, bias: torch.Tensor, ksize: int, stride: int, transposed: bool, device):
+        import ctypes
+        lib = _lib.load()
+        w = weight.detach().to("cpu", torch.float32).contiguous()
+        cin, cout = (w.shape[0], w.shape[1]) if transposed else (w.shape[1], w.shape[0])
+        if cout > 4 or ksize not in (3, 5) or stride != (2 if transposed else 1):
+            raise ValueError("tap form needs cout <= 4, k 3/5, conv stride 1 or transposed stride 2")
+        self.cin, self.cout, self.ksize, self.stride, self.transposed = cin, cout, ksize, stride, transposed
+        nt = ksize * ksize
+        wt = w.permute(2, 3, 1, 0) if transposed else w.permute(2, 3, 0, 1)  # [ky][kx][co][ci]
+        wt = wt.reshape(nt * cout, cin).contiguous()
+        self.np, self.pcp = nt * cout, cp4(nt * cout)
+        nbytes = lib.fvc_x3_tap_wpack_bytes(self.np, cin)
+        if nbytes == 0:
+            raise ValueError(f"tap form unsupported: {self.np} partials from {cin} channels")
+        packed = torch.empty(nbytes // 2, dtype=torch.float16)
+        osc = ctypes.c_float(0.0)
+        _lib.call("fvc_x3_tap_pack_weight", wt.data_ptr(), packed.data_ptr(), ctypes.addressof(osc), self.np, cin)
+        self.osc = float(osc.value)
+        self.wpack = packed.to(device)
+        self.bias = bias.detach().to(device, torch.float32).contiguous()
+
+    def gather(self, P, act=ACT_NONE, post=POST_NONE, res=None):
+        B, H, W, pcp = P.shape
+        if pcp != self.pcp:
+            raise ValueError(f"P has {pcp} channels, expected {self.pcp}")
+        _chk(P, name="P")
+        ho, wo = (H * self.stride, W * self.stride) if self.transposed else (H, W)
+        y = torch.empty((B, ho, wo, cp4(self.cout)), dtype=torch.float32, device=P.device)
+        _chk(res, y.shape, name="res")
+        nb = 4 * (P.numel() + y.numel() * (2 if res is not None else 1))
+        profiling.timed_hbm("tap_gather", nb, lambda: _lib.call(
+            "fvc_tap_gather_nhwc", P.data_ptr(), pcp, self.bias.data_ptr(), _ptr(res), y.data_ptr(), B, H, W,
+            self.cout, self.ksize, self.stride, int(self.transposed), act, post, stream_handle()))
+        return y
+
+
 def x3_overflow(reset: bool = True, device=None) -> bool:
     """True if any split-precision conv on the current stream staged an activation with
     |v| >= 65000 since the last reset (waits for the stream's queued work)."""

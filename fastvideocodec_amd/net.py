@@ -18,6 +18,8 @@ coder (the reference's DVC path only estimates bits unless ``calrealbits``, net.
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
 import torch.nn as nn
@@ -51,8 +53,33 @@ class _ConvP(nn.Module):
                                            self.weight.device, precision=p)
         return self._packed[p]
 
+    def tap_consumer(self):
+        """This (cout <= 4) layer in tap-partial form for fusion into its producer (cached), or
+        None when it has more than 32 partials (k*k*cout)."""
+        if "tap" not in self._packed:
+            try:
+                self._packed["tap"] = K.TapConsumer(self.weight, self.bias, self.k, self.stride, self.transposed,
+                                                    self.weight.device)
+            except ValueError:
+                self._packed["tap"] = None
+        return self._packed["tap"]
+
     def invalidate(self):
         self._packed = {}
+
+
+def conv_then_tap(prod: _ConvP, x, cons: _ConvP, act=K.ACT_NONE, res=None, cons_act=K.ACT_NONE,
+                  cons_res=None):
+    """cons(prod(x, act, res), cons_act, cons_res) for a cout <= 4 consumer: on the split-precision
+    path the consumer's 1x1 tap-partial GEMM runs in the producer's epilogue (the producer's
+    output never reaches HBM; fvc_conv2d_nhwc_x3_tap + fvc_tap_gather_nhwc), else two layers.
+    FVC_TAP_FUSE=0 disables the fusion (A/B and tests)."""
+    p = prod.packed()
+    if K.conv_precision() == "x3" and os.environ.get("FVC_TAP_FUSE", "1") != "0":
+        t = cons.tap_consumer()
+        if t is not None and p.tap_fusable(t):
+            return t.gather(p.call_tap(x, t, act=act, res=res), act=cons_act, res=cons_res)
+    return cons.packed()(p(x, act=act, res=res), act=cons_act, res=cons_res)
 
 
 class _GDNP(nn.Module):
@@ -175,10 +202,11 @@ class Synthesis_mv_net(nn.Module):
 
     def run(self, q):
         x = q
-        for i in range(1, 9):
+        for i in range(1, 7):
             x = getattr(self, f"deconv{i}").packed()(x, in_op=K.IN_ROUND if i == 1 else K.IN_NONE,
-                                                     act=K.ACT_LRELU if i < 8 else K.ACT_NONE)
-        return x
+                                                     act=K.ACT_LRELU)
+        # deconv7 (128 ch at full resolution) feeds only the 128->2 deconv8: fused
+        return conv_then_tap(self.deconv7, x, self.deconv8, act=K.ACT_LRELU)
 
 
 class ResBlock(nn.Module):
@@ -213,8 +241,10 @@ class Warp_net(nn.Module):
         c3u = K.upsample2x_add(c3, skip=c1, align_corners=True)
         c4 = self.conv4.run(c3u)
         c4u = K.upsample2x_add(c4, skip=c0, align_corners=True)
-        c5 = self.conv5.run(c4u)
-        return self.conv6.packed()(c5, res=warpframe)  # prediction = warpnet(...) + warpframe (net.py:67)
+        # c5 = conv5(c4u) feeds only conv6 (64->3): its second conv runs fused with conv6's taps;
+        # prediction = warpnet(...) + warpframe (net.py:67)
+        y = self.conv5.conv1.packed()(c4u, in_op=K.IN_RELU, act=K.ACT_RELU)
+        return conv_then_tap(self.conv5.conv2, y, self.conv6, res=c4u, cons_res=warpframe)
 
 
 class Analysis_net(nn.Module):

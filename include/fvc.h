@@ -104,6 +104,27 @@ int fvc_deconv2d_nhwc_x3(const float* x, const void* wpack, float osc, const flo
                          const float* res, float* y, int batch, int h, int w, int cin, int cout,
                          int ksize, int stride, int in_op, int act, int post_op, int cu_reserve,
                          int* overflow_flag, int* sched, int sched_len, fvc_stream_t stream);
+/* Fused producer + tap partials of a cout <= 4 consumer (the pair nn.Conv2d(c->128/64) ->
+ * nn.Conv2d(128/64->2/3): synthesis_mv.py:41-43 deconv7 -> deconv8, endecoder.py:278-279
+ * Warp_net conv5 -> conv6): the producer conv / transposed conv runs as fvc_*_x3 (in_op none,
+ * act, res; post none) but instead of its output y it writes
+ *   P [batch][Ho][Wo][pcp] = tap_w [np][cout] . y   per output pixel   (np <= pcp <= 32)
+ * i.e. the 1x1 first half of the consumer's tap-partial form, which fvc_tap_gather_nhwc then
+ * sums into the consumer's output. tap_wpack from fvc_x3_tap_pack_weight (host), np = k*k*cout'
+ * rows t*cout' + co. fvc_conv_x3_tap_supported says whether a geometry takes this path. */
+int fvc_conv_x3_tap_supported(int cin, int cout, int ksize, int stride, int transposed, int pcp);
+size_t fvc_x3_tap_wpack_bytes(int np, int cin);
+int fvc_x3_tap_pack_weight(const float* w_host, void* wpack_host, float* osc_out, int np, int cin);
+int fvc_conv2d_nhwc_x3_tap(const float* x, const void* wpack, float osc, const float* bias,
+                           const float* res, float* P, int batch, int h, int w, int cin, int cout,
+                           int ksize, int stride, int act, const void* tap_wpack, float tap_osc,
+                           int pcp, int cu_reserve, int* overflow_flag, int* sched, int sched_len,
+                           fvc_stream_t stream);
+int fvc_deconv2d_nhwc_x3_tap(const float* x, const void* wpack, float osc, const float* bias,
+                             const float* res, float* P, int batch, int h, int w, int cin, int cout,
+                             int ksize, int stride, int act, const void* tap_wpack, float tap_osc,
+                             int pcp, int cu_reserve, int* overflow_flag, int* sched, int sched_len,
+                             fvc_stream_t stream);
 
 /* ------------------------------------------------------------------ layout / resampling */
 int fvc_nchw_to_nhwc(const float* src, float* dst, int batch, int c, int h, int w, int cp,

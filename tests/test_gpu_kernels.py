@@ -144,6 +144,64 @@ def test_conv_tap_partial_path(dev, case, monkeypatch):
     assert float(yc[..., cout:].abs().max()) == 0.0
 
 
+# (producer cin, cout, k, stride, transposed, act, with_res, consumer cout, k, H, W, batch)
+TAP_FUSE_CASES = [
+    (128, 128, 3, 2, True, K.ACT_LRELU, False, 2, 3, 9, 21, 2),    # mvDecoder deconv7 -> deconv8
+    (64, 64, 3, 1, False, K.ACT_NONE, True, 3, 3, 19, 45, 2),      # Warp_net conv5.conv2 -> conv6
+    (64, 64, 3, 1, False, K.ACT_RELU, False, 2, 5, 17, 33, 1),     # 5x5 consumer, 50 partials > 32: refused
+    (32, 32, 3, 1, False, K.ACT_NONE, True, 3, 3, 16, 40, 3),      # one N-tile producer
+]
+
+
+@pytest.mark.parametrize("case", TAP_FUSE_CASES, ids=lambda c: f"p{c[0]}-{c[1]}k{c[2]}{'T' if c[4] else ''}-c{c[7]}k{c[8]}")
+def test_conv_then_tap_fused(dev, case, monkeypatch):
+    """Producer conv with the consumer's 1x1 tap-partial GEMM in its epilogue
+    (fvc_*_x3_tap + fvc_tap_gather_nhwc) against the fp32 torch pair, and against the unfused
+    two-layer path (FVC_TAP_FUSE=0)."""
+    from fastvideocodec_amd import net
+    ci, co, k, s, tr, act, with_res, c2, k2, H, W, B = case
+    g = torch.Generator().manual_seed(ci + 7 * co + k2)
+    x = torch.randn(B, ci, H, W, generator=g)
+    w1 = torch.randn((ci, co, k, k) if tr else (co, ci, k, k), generator=g) * (1.0 / (ci * k * k) ** 0.5)
+    b1 = torch.randn(co, generator=g) * 0.1
+    w2 = torch.randn(c2, co, k2, k2, generator=g) * (1.0 / (co * k2 * k2) ** 0.5)
+    b2 = torch.randn(c2, generator=g) * 0.1
+    y = F.conv_transpose2d(x, w1, b1, s, k // 2, s - 1) if tr else F.conv2d(x, w1, b1, s, k // 2)
+    y = {K.ACT_NONE: y, K.ACT_RELU: F.relu(y), K.ACT_LRELU: F.leaky_relu(y, 0.1)}[act]
+    res = torch.randn(y.shape, generator=g) if with_res else None
+    if res is not None:
+        y = y + res
+    ref = F.conv2d(y, w2, b2, 1, k2 // 2)
+    res2 = torch.randn(ref.shape, generator=g)
+    ref = ref + res2
+
+    prod = net._ConvP(ci, co, k, s, tr)
+    prod.weight.data.copy_(w1)
+    prod.bias.data.copy_(b1)
+    cons = net._ConvP(co, c2, k2, 1, False)
+    cons.weight.data.copy_(w2)
+    cons.bias.data.copy_(b2)
+    prod.to(dev)
+    cons.to(dev)
+    xd = to_nhwc(x).to(dev)
+    rd = None if res is None else to_nhwc(res).to(dev)
+    r2d = to_nhwc(res2).to(dev)
+    t = cons.tap_consumer()
+    fusable = t is not None and prod.packed().tap_fusable(t)
+    assert fusable == (c2 * k2 * k2 <= 32), "fusion must cover exactly the <= 32-partial consumers"
+    K.x3_overflow(reset=True)
+    out = net.conv_then_tap(prod, xd, cons, act=act, res=rd, cons_res=r2d)
+    torch.cuda.synchronize()
+    assert not K.x3_overflow(reset=True)
+    oc = out.cpu()
+    close(from_nhwc(oc, c2), ref, 2e-5)
+    assert float(oc[..., c2:].abs().max()) == 0.0
+    monkeypatch.setenv("FVC_TAP_FUSE", "0")
+    out2 = net.conv_then_tap(prod, xd, cons, act=act, res=rd, cons_res=r2d)
+    torch.cuda.synchronize()
+    close(from_nhwc(out2.cpu(), c2), from_nhwc(oc, c2), 2e-6)
+
+
 @pytest.mark.parametrize("wn", ["1", "2", "4"])
 def test_conv_x3_ntile_groupings(dev, wn, monkeypatch):
     """The stride-2 128->128 conv with 1, 2 or all 4 N-tiles per block (FVC_X3_WN; 4 is the
