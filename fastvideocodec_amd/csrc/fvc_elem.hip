@@ -95,6 +95,129 @@ __global__ __launch_bounds__(256) void k_tap_gather(const float* __restrict__ P,
   }
 }
 
+// Stride-1 3x3 tap gather through LDS (the second half of the fused producer + tap path): a block
+// stages the P tile of its 16 x 32 outputs plus a 1-pixel halo with coalesced 16-B loads (zeros
+// outside the image), pixel stride pcp + 1 words so the per-tap reads of consecutive outputs hit
+// distinct banks, then sums bias + taps in k_tap_gather's order (an out-of-image tap adds +0).
+template <int COUT>
+__global__ __launch_bounds__(256) void k_tap_gather3_lds(const float* __restrict__ P, int pcp,
+                                                         const float* __restrict__ bias,
+                                                         const float* __restrict__ res, float* __restrict__ y,
+                                                         int H, int W, float act_slope, int post_op) {
+  constexpr int TH = 16, TW = 32, IR = TH + 2, IC = TW + 2;
+  extern __shared__ float sp[];
+  const int ps = pcp + 1;
+  const int c4n = pcp >> 2;
+  const size_t b = blockIdx.z;
+  const int y0 = blockIdx.y * TH, x0 = blockIdx.x * TW;
+  const float* Pb = P + b * H * W * pcp;
+  for (int e = threadIdx.x; e < IR * IC * c4n; e += blockDim.x) {
+    const int c4 = e % c4n, p = e / c4n;
+    const int iy = y0 - 1 + p / IC, ix = x0 - 1 + p % IC;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if ((unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W)
+      v = *reinterpret_cast<const float4*>(Pb + ((size_t)iy * W + ix) * pcp + 4 * c4);
+    float* d = sp + p * ps + 4 * c4;
+    d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+  }
+  __syncthreads();
+  for (int q = threadIdx.x; q < TH * TW; q += blockDim.x) {
+    const int r = q / TW, c = q % TW;
+    const int Y = y0 + r, X = x0 + c;
+    if (Y >= H || X >= W) continue;
+    float acc[COUT];
+#pragma unroll
+    for (int co = 0; co < COUT; ++co) acc[co] = bias[co];
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) {
+        const float* src = sp + ((r + ky) * IC + c + kx) * ps + (ky * 3 + kx) * COUT;
+#pragma unroll
+        for (int co = 0; co < COUT; ++co) acc[co] += src[co];
+      }
+    const size_t e = (b * H + Y) * W + X;
+    float4 rv = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (res) rv = reinterpret_cast<const float4*>(res)[e];
+    const float rr[4] = {rv.x, rv.y, rv.z, rv.w};
+    float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
+    float* ov = &o.x;
+#pragma unroll
+    for (int co = 0; co < COUT; ++co) {
+      float v = acc[co];
+      v = fmaxf(v, v * act_slope);
+      if (res) v += rr[co];
+      if (post_op == FVC_POST_EXP) v = expf(v);
+      ov[co] = v;
+    }
+    reinterpret_cast<float4*>(y)[e] = o;
+  }
+}
+
+// Transposed (stride 2, output padding 1) tap gather through LDS: a block's 16 x 32 outputs read
+// input rows Y0/2 - 1 .. Y0/2 + 8 and columns X0/2 - 1 .. X0/2 + 17 of P (k = 3 or 5), staged
+// once with coalesced 16-B loads; per output the same tap order as k_tap_gather.
+template <int KS, int COUT>
+__global__ __launch_bounds__(256) void k_tap_gather_t2_lds(const float* __restrict__ P, int pcp,
+                                                           const float* __restrict__ bias,
+                                                           const float* __restrict__ res, float* __restrict__ y,
+                                                           int H, int W, float act_slope, int post_op) {
+  constexpr int TH = 16, TW = 32, IR = 10, IC = 19, pad = KS / 2;
+  extern __shared__ float sp[];
+  const int ps = pcp + 1;
+  const int c4n = pcp >> 2;
+  const int Ho = 2 * H, Wo = 2 * W;
+  const size_t b = blockIdx.z;
+  const int Y0 = blockIdx.y * TH, X0 = blockIdx.x * TW;
+  const int r0 = Y0 / 2 - 1, c0 = X0 / 2 - 1;
+  const float* Pb = P + b * H * W * pcp;
+  for (int e = threadIdx.x; e < IR * IC * c4n; e += blockDim.x) {
+    const int c4 = e % c4n, p = e / c4n;
+    const int iy = r0 + p / IC, ix = c0 + p % IC;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if ((unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W)
+      v = *reinterpret_cast<const float4*>(Pb + ((size_t)iy * W + ix) * pcp + 4 * c4);
+    float* d = sp + p * ps + 4 * c4;
+    d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+  }
+  __syncthreads();
+  for (int q = threadIdx.x; q < TH * TW; q += blockDim.x) {
+    const int Y = Y0 + q / TW, X = X0 + q % TW;
+    if (Y >= Ho || X >= Wo) continue;
+    float acc[COUT];
+#pragma unroll
+    for (int co = 0; co < COUT; ++co) acc[co] = bias[co];
+#pragma unroll
+    for (int ky = 0; ky < KS; ++ky) {
+      if ((Y + pad - ky) & 1) continue;
+      const int lr = ((Y + pad - ky) >> 1) - r0;  // in [0, IR): out-of-image rows hold zeros
+#pragma unroll
+      for (int kx = 0; kx < KS; ++kx) {
+        if ((X + pad - kx) & 1) continue;
+        const int lc = ((X + pad - kx) >> 1) - c0;
+        const float* src = sp + (lr * IC + lc) * ps + (ky * KS + kx) * COUT;
+#pragma unroll
+        for (int co = 0; co < COUT; ++co) acc[co] += src[co];
+      }
+    }
+    const size_t e = (b * Ho + Y) * Wo + X;
+    float4 rv = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (res) rv = reinterpret_cast<const float4*>(res)[e];
+    const float rr[4] = {rv.x, rv.y, rv.z, rv.w};
+    float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
+    float* ov = &o.x;
+#pragma unroll
+    for (int co = 0; co < COUT; ++co) {
+      float v = acc[co];
+      v = fmaxf(v, v * act_slope);
+      if (res) v += rr[co];
+      if (post_op == FVC_POST_EXP) v = expf(v);
+      ov[co] = v;
+    }
+    reinterpret_cast<float4*>(y)[e] = o;
+  }
+}
+
 __global__ void k_avgpool2(const float* __restrict__ src, float* __restrict__ dst, int B, int H, int W,
                            int cp) {
   const int Ho = H / 2, Wo = W / 2, c4n = cp / 4;
@@ -738,6 +861,38 @@ int fvc_tap_gather_nhwc(const float* P, int pcp, const float* bias, const float*
   const size_t n = (size_t)batch * Ho * Wo;
   const dim3 g(grid_for(n)), bl(kBlk);
   hipStream_t st = (hipStream_t)s;
+  if (!transposed && ksize == 3 && pcp <= 32) {
+    const dim3 gt(fvc_cdiv(w, 32), fvc_cdiv(h, 16), batch);
+    const size_t lds = (size_t)18 * 34 * (pcp + 1) * 4;
+#define FVC_TGL(CO)                                                                                             \
+    if (cout == CO) {                                                                                         \
+      if (lds > 64 * 1024)                                                                                    \
+        (void)hipFuncSetAttribute((const void*)k_tap_gather3_lds<CO>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+                                  (int)lds);                                                                  \
+      hipLaunchKernelGGL((k_tap_gather3_lds<CO>), gt, dim3(256), lds, st, P, pcp, bias, res, y, h, w, slope, post_op); \
+      FVC_CHECK_LAUNCH();                                                                                     \
+      return 0;                                                                                               \
+    }
+    FVC_TGL(1) FVC_TGL(2) FVC_TGL(3) FVC_TGL(4)
+#undef FVC_TGL
+  }
+  if (transposed && pcp <= 128) {
+    const dim3 gt(fvc_cdiv(Wo, 32), fvc_cdiv(Ho, 16), batch);
+    const size_t lds = (size_t)10 * 19 * (pcp + 1) * 4;
+#define FVC_TGT(KS, CO)                                                                                        \
+    if (ksize == KS && cout == CO) {                                                                          \
+      if (lds > 64 * 1024)                                                                                    \
+        (void)hipFuncSetAttribute((const void*)k_tap_gather_t2_lds<KS, CO>,                                   \
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                      \
+      hipLaunchKernelGGL((k_tap_gather_t2_lds<KS, CO>), gt, dim3(256), lds, st, P, pcp, bias, res, y, h, w, slope, \
+                         post_op);                                                                            \
+      FVC_CHECK_LAUNCH();                                                                                     \
+      return 0;                                                                                               \
+    }
+    FVC_TGT(3, 1) FVC_TGT(3, 2) FVC_TGT(3, 3) FVC_TGT(3, 4)
+    FVC_TGT(5, 1) FVC_TGT(5, 2) FVC_TGT(5, 3) FVC_TGT(5, 4)
+#undef FVC_TGT
+  }
 #define FVC_TG(KS, CO, TR)                                                                                   \
   if (ksize == KS && cout == CO && transposed == TR) {                                                       \
     hipLaunchKernelGGL((k_tap_gather<KS, CO, TR>), g, bl, 0, st, P, pcp, bias, res, y, batch, h, w, Ho, Wo, \

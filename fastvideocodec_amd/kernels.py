@@ -247,11 +247,12 @@ class PackedConv:
         precision = precision or conv_precision()
         self.cin, self.cout, self.ksize, self.stride, self.transposed = cin, cout, ksize, stride, transposed
         # cout <= 4 with a wide input (mvDecoder deconv8, 128->2 3x3): N padded to a 32-wide MFMA
-        # tile wastes 16x, so the layer runs as a 1x1 x3 GEMM to N' = k*k*cout tap partials per
-        # input pixel + fvc_tap_gather_nhwc (0.66 -> 0.47 ms at 1080p). For 64 input channels
-        # (Warp_net conv6, resDecoder deconv4) the direct x3 kernel is faster (0.31 vs 0.43 ms,
-        # 0.24 vs 0.35 ms), so they stay direct. FVC_TAPSUM=0 / 2 disables / forces the tap path
-        # for every eligible layer.
+        # tile wastes 16x, so the layer can run as a 1x1 x3 GEMM to N' = k*k*cout tap partials per
+        # input pixel + the LDS-tiled fvc_tap_gather_nhwc (net.py normally fuses the partial GEMM
+        # into the producer instead: conv_then_tap, for deconv8 and Warp_net conv6). resDecoder
+        # deconv4 (64->3 5x5 s2) stays direct: 1x1 GEMM 0.57 + gather 0.45 ms vs 0.86 ms direct
+        # per 4-frame launch (MI355X, r2). FVC_TAPSUM=0 / 2 disables / forces the tap path for
+        # every eligible layer.
         self.tap = None
         tapsum = os.environ.get("FVC_TAPSUM", "1")
         if (precision == "x3" and cout <= 4 and ksize in (3, 5) and stride == (2 if transposed else 1)
