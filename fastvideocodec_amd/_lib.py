@@ -30,6 +30,8 @@ _SIGS = {
     "fvc_conv2d_nhwc_x3": (c_int, [vp, vp, c_float, vp, vp, vp] + [c_int] * 11 + [vp, vp, c_int, vp]),
     "fvc_deconv2d_nhwc_x3": (c_int, [vp, vp, c_float, vp, vp, vp] + [c_int] * 11 + [vp, vp, c_int, vp]),
     "fvc_conv_x3_tap_supported": (c_int, [c_int] * 6),
+    "fvc_conv_x3_pool_supported": (c_int, [c_int] * 3),
+    "fvc_conv2d_nhwc_x3_pool": (c_int, [vp, vp, c_float, vp, vp, vp, vp] + [c_int] * 8 + [vp, vp, c_int, vp]),
     "fvc_x3_tap_wpack_bytes": (c_size_t, [c_int, c_int]),
     "fvc_x3_tap_pack_weight": (c_int, [vp, vp, vp, c_int, c_int]),
     "fvc_conv2d_nhwc_x3_tap": (c_int, [vp, vp, c_float, vp, vp, vp] + [c_int] * 8 + [vp, c_float]

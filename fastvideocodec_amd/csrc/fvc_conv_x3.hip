@@ -83,6 +83,8 @@ constexpr int kNPL = kAcc1 ? 3 : 2;        // weight planes per (k-step, N-tile)
 constexpr int kFrag = 64 * kNPL;          // uint4 per (k-step, N-tile)
 // internal post-op of the fused tap path (fvc_conv2d_nhwc_x3_tap): not part of the public enum
 constexpr int kPostTap = 2;
+// internal post-op of fvc_conv2d_nhwc_x3_pool: y and its 2x2 average pool (stride-1 convs, WM = 2)
+constexpr int kPostPool = 3;
 
 struct X3Args {
   const float* x;
@@ -119,6 +121,9 @@ struct X3Args {
   const uint4* tw;                 // tap weights [k16 block][hi|lo][lane] (fvc_x3_tap_pack_weight)
   float tosc, tosc_c;              // 2^-kt, 2^-kt-11
   int pcp;                         // P channels (partials rounded up to 4, <= 32)
+  // POST == kPostPool: the epilogue also writes avg_pool2d(y) (2x2, stride 2) to pool
+  float* pool;
+  unsigned pool_bytes;
   int toff[4][kMaxTapsX + 1];      // LDS offset (halves) of each tap's window; 0 past ntaps
 };
 
@@ -690,6 +695,16 @@ __global__ __launch_bounds__(NWV * 64) void conv_x3_kernel(const X3Args a) {
         r[g] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rr, vo + 32u * g, 0, 0));
     };
     if (a.res && kResPipe) load_res(0, rv[0]);
+    // kPostPool: strips 0 and 1 of a wave are output rows 2r and 2r+1 and lanes li, li^1 are
+    // columns 2c, 2c+1, so each 2x2 window is in one wave: strip 0's values are kept, strip 1
+    // adds them with a DPP quad swap, and the even lanes store the pooled pixel (ATen order
+    // ((x00 + x01) + x10) + x11, / 4: the same bits as k_avgpool2)
+    float keep[POST == kPostPool ? WN : 1][4][4];
+    const __amdgpu_buffer_rsrc_t rpool =
+        __builtin_amdgcn_make_buffer_rsrc((void*)a.pool, (short)0, (int)a.pool_bytes, kRsrcFlags);
+    auto swap1 = [](float x) {  // value of lane li ^ 1 (quad_perm [1, 0, 3, 2])
+      return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0xB1, 0xF, 0xF, false));
+    };
 #pragma unroll
     for (int t = 0; t < NTL; ++t) {
       const int m = t / WN, n = t % WN;
@@ -724,6 +739,39 @@ __global__ __launch_bounds__(NWV * 64) void conv_x3_kernel(const X3Args a) {
         const unsigned so = (row_ok && j0 < a.coutp) ? vo + 32u * g : kOob;
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, make_float4(v[0], v[1], v[2], v[3])),
                                                ry, so, 0, 0);
+        if constexpr (POST == kPostPool) {
+          if (m == 0) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) keep[n][g][i] = v[i];
+          } else {
+            // pooled values on the even lanes; groups g (even) and g + 1 go out in one store: the
+            // odd lane li + 1 takes group g + 1 of its even neighbour (channels 8 further)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const float x00 = keep[n][g][i], x10 = v[i];
+              keep[n][g][i] = (((x00 + swap1(x00)) + x10) + swap1(x10)) / 4.f;
+            }
+            if (g & 1) {
+              // the swap runs on every lane (a DPP read from a lane switched off by a branch
+              // would return 0), then a bitwise select keeps the branch out
+              float pv[4];
+              const int odd = -(li & 1);
+#pragma unroll
+              for (int i = 0; i < 4; ++i) {
+                const int sw = __builtin_bit_cast(int, swap1(keep[n][g][i]));
+                const int ev = __builtin_bit_cast(int, keep[n][g - 1][i]);
+                pv[i] = __builtin_bit_cast(float, (sw & odd) | (ev & ~odd));
+              }
+              const int Hp = a.Hq >> 1, Wp = a.Wq >> 1;
+              const int prow = (qy0 + wm_ * WM) >> 1, pcol = (qx0 + li) >> 1;
+              const int jp = (ntw + n) * 32 + 8 * (g - 1 + (li & 1)) + 4 * lh;  // this lane's channels
+              const bool pok = prow < Hp && pcol < Wp && jp < a.coutp;
+              const unsigned po = (((unsigned)b * Hp + prow) * Wp + pcol) * (unsigned)a.coutp * 4u + (unsigned)jp * 4u;
+              __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, make_float4(pv[0], pv[1], pv[2], pv[3])),
+                                                     rpool, pok ? po : kOob, 0, 0);
+            }
+          }
+        }
       }
     }
     TR(5);
@@ -913,6 +961,11 @@ static int x3_launch(const X3Args& a, dim3 grid, size_t lds, hipStream_t s) {
 // deconv3, synthesis_prior.py:25,57): instantiated for IN_NONE only
 template <int CC, int WM, int WN, int WG, int WL, int NWV = 8>
 static int x3_launch_iop(int iop, int post, const X3Args& a, dim3 grid, size_t lds, hipStream_t s) {
+  if (post == kPostPool) {  // fused 2x2 pool epilogue: strip pairs per wave (run_x3)
+    if constexpr (WG == 1 && WL == 0 && WM == 2 && WN <= 2)
+      return iop == FVC_IN_NONE ? x3_launch<CC, WM, WN, WG, FVC_IN_NONE, kPostPool, NWV, WL>(a, grid, lds, s) : FVC_EINVAL;
+    return FVC_EINVAL;
+  }
   if (post == kPostTap) {  // fused tap epilogue: every output channel in one wave (run_x3)
     if constexpr (WG == 1 && WL == 0 && ((WM == 2 && WN <= 2) || (WM == 1 && WN == 4)))
       return iop == FVC_IN_NONE ? x3_launch<CC, WM, WN, WG, FVC_IN_NONE, kPostTap, NWV, WL>(a, grid, lds, s) : FVC_EINVAL;
@@ -948,7 +1001,7 @@ static int x3_launch_cc(int nwv, int wm, int wn, int wg, int iop, int post, cons
 static int run_x3(const float* x, const void* wpack, float osc, const float* bias, const float* res,
                   float* y, int batch, int h, int w, int cin, int cout, int ks, int stride, int transposed,
                   int in_op, int act, int post_op, int cu_reserve, int* ovf, int* sched, int sched_len,
-                  hipStream_t s, const void* tw = nullptr, float tosc = 0.f, int pcp = 0) {
+                  hipStream_t s, const void* tw = nullptr, float tosc = 0.f, int pcp = 0, float* pool = nullptr) {
   X3Cfg c;
   if (!x3_cfg(cin, cout, ks, stride, transposed, c)) return FVC_EINVAL;
   if (!x || !wpack || !bias || !y || batch <= 0 || h <= 0 || w <= 0) return FVC_EINVAL;
@@ -961,6 +1014,13 @@ static int run_x3(const float* x, const void* wpack, float osc, const float* bia
     if (c.ntp == 4) c.wm = 1;
     c.th = c.nw * c.wm;
     post_op = kPostTap;
+  }
+  if (pool) {
+    // y and avg_pool2d(y): stride-1 conv, two strips per wave (rows 2r, 2r + 1), one N-group
+    if (tw || transposed || stride != 1 || post_op != FVC_POST_NONE || in_op != FVC_IN_NONE || c.wl || c.wm != 2 ||
+        c.ntp > 2)
+      return FVC_EINVAL;
+    post_op = kPostPool;
   }
   const int ych = tw ? pcp : c.coutp;  // channels of the tensor y points to
   X3Args a;
@@ -987,15 +1047,19 @@ static int run_x3(const float* x, const void* wpack, float osc, const float* bia
     if (batch == 1) return FVC_EINVAL;
     const int b1 = batch / 2;
     const size_t xs = (size_t)h * w * c.cinp, ys = (size_t)a.Ho * a.Wo * ych, rs = (size_t)a.Ho * a.Wo * c.coutp;
-    const int post_in = tw ? FVC_POST_NONE : post_op;
+    const int post_in = (tw || pool) ? FVC_POST_NONE : post_op;
+    const size_t pls = (size_t)(a.Ho / 2) * (a.Wo / 2) * c.coutp;
     int rc = run_x3(x, wpack, osc, bias, res, y, b1, h, w, cin, cout, ks, stride, transposed, in_op, act,
-                    post_in, cu_reserve, ovf, sched, sched_len, s, tw, tosc, pcp);
+                    post_in, cu_reserve, ovf, sched, sched_len, s, tw, tosc, pcp, pool);
     if (rc) return rc;
     return run_x3(x + b1 * xs, wpack, osc, bias, res ? res + b1 * rs : nullptr, y + b1 * ys, batch - b1, h, w, cin, cout, ks,
-                  stride, transposed, in_op, act, post_in, cu_reserve, ovf, sched, sched_len, s, tw, tosc, pcp);
+                  stride, transposed, in_op, act, post_in, cu_reserve, ovf, sched, sched_len, s, tw, tosc, pcp,
+                  pool ? pool + b1 * pls : nullptr);
   }
   a.y_bytes = (unsigned)ybytes;
   a.res_bytes = (unsigned)rbytes;
+  a.pool = pool;
+  a.pool_bytes = (unsigned)((unsigned long long)batch * (a.Ho / 2) * (a.Wo / 2) * c.coutp * 4ull);
   // the input is addressed per image (blockIdx.z) through a 32-bit-range descriptor too
   const unsigned long long xbytes = (unsigned long long)h * w * c.cinp * 4ull;
   if (xbytes >= (1ull << 32) - 4096) return FVC_EINVAL;
@@ -1042,17 +1106,17 @@ static int run_x3(const float* x, const void* wpack, float osc, const float* bia
   // stride-2 convs (one strip per wave) with 4 N-tiles take all 128 channels per block: the
   // input tile is staged once instead of twice (3x3 s2 128->128 at 544x960: 0.214 -> 0.191 ms)
   int wn = (c.wm == 1 && !transposed && stride == 2 && c.ntp % 4 == 0) ? 4 : (c.ntp >= 2 ? 2 : 1);
-  const int want_wn = tw ? c.ntp : env_int("FVC_X3_WN", 0);
+  const int want_wn = (tw || pool) ? c.ntp : env_int("FVC_X3_WN", 0);
   if (want_wn == 1 || want_wn == 2 || (want_wn == 4 && c.wm == 1)) wn = want_wn;
   while (wn > 1 && c.ntp % wn) wn >>= 1;
   const long long base = (long long)tiles_x * tiles_y * batch * c.nclass;
   if (!want_wn)
     while (wn > 1 && base * (c.ntp / wn) < 2LL * x3_num_cus()) wn >>= 1;
-  if (tw && wn != c.ntp) return FVC_EINVAL;
+  if ((tw || pool) && wn != c.ntp) return FVC_EINVAL;
   // two N-groups of 4 waves x 4 strips instead of 8 waves x 2 strips x 2 N-tiles (same block
   // tile: 16 rows x 32 pixels x 64 channels): each weight fragment feeds 4 strips
   int wm = c.wm, wg = 1;
-  if (c.nw == 8 && !c.wl && !tw && env_int("FVC_X3_WG", 0) == 2 && c.wm == 2 && wn == 2) {
+  if (c.nw == 8 && !c.wl && !tw && !pool && env_int("FVC_X3_WG", 0) == 2 && c.wm == 2 && wn == 2) {
     wm = 4;
     wn = 1;
     wg = 2;
@@ -1225,6 +1289,19 @@ int fvc_deconv2d_nhwc_x3_tap(const float* x, const void* wpack, float osc, const
   return run_x3(x, wpack, osc, bias, res, P, batch, h, w, cin, cout, ksize, stride, 1, FVC_IN_NONE, act,
                 FVC_POST_NONE, cu_reserve, overflow_flag, sched, sched_len, (hipStream_t)stream, tap_wpack, tap_osc,
                 pcp);
+}
+
+int fvc_conv_x3_pool_supported(int cin, int cout, int ksize) {
+  X3Cfg c;
+  return x3_cfg(cin, cout, ksize, 1, 0, c) && !c.wl && c.wm == 2 && c.ntp <= 2;
+}
+
+int fvc_conv2d_nhwc_x3_pool(const float* x, const void* wpack, float osc, const float* bias, const float* res,
+                            float* y, float* pool, int batch, int h, int w, int cin, int cout, int ksize, int act,
+                            int cu_reserve, int* overflow_flag, int* sched, int sched_len, fvc_stream_t stream) {
+  if (cu_reserve < 0 || sched_len < 0 || !pool || !fvc_conv_x3_pool_supported(cin, cout, ksize)) return FVC_EINVAL;
+  return run_x3(x, wpack, osc, bias, res, y, batch, h, w, cin, cout, ksize, 1, 0, FVC_IN_NONE, act, FVC_POST_NONE,
+                cu_reserve, overflow_flag, sched, sched_len, (hipStream_t)stream, nullptr, 0.f, 0, pool);
 }
 
 int fvc_conv2d_nhwc_x3(const float* x, const void* wpack, float osc, const float* bias,

@@ -333,6 +333,38 @@ class PackedConv:
         return y
 
 
+    def pool_fusable(self) -> bool:
+        return (self.x3 and self.tap is None and not self.transposed and self.stride == 1 and
+                bool(_lib.load().fvc_conv_x3_pool_supported(self.cin, self.cout, self.ksize)))
+
+    def call_pool(self, x, act=ACT_NONE, res=None):
+        """(y, avg_pool2d(y, 2)) from one launch (fvc_conv2d_nhwc_x3_pool; in_op none, post none)."""
+        if not self.pool_fusable():
+            raise ValueError("conv not poolable in its epilogue")
+        B, H, W, cp = x.shape
+        if cp != cp4(self.cin):
+            raise ValueError(f"conv input has {cp} channels, expected {cp4(self.cin)}")
+        _chk(x, name="x")
+        oshape = (B, H, W, cp4(self.cout))
+        _chk(res, oshape, name="res")
+        y = torch.empty(oshape, dtype=torch.float32, device=x.device)
+        pool = torch.empty((B, H // 2, W // 2, cp4(self.cout)), dtype=torch.float32, device=x.device)
+        timer = profiling.active()
+        if timer is not None:
+            ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            ev0.record()
+        _lib.call("fvc_conv2d_nhwc_x3_pool", x.data_ptr(), self.wpack.data_ptr(), self.osc, self.bias.data_ptr(),
+                  _ptr(res), y.data_ptr(), pool.data_ptr(), B, H, W, self.cin, self.cout, self.ksize, act,
+                  _STATE["cu_reserve"], overflow_flag(x.device).data_ptr(), sched_scratch(x.device).data_ptr(),
+                  SCHED_LEN, stream_handle())
+        if timer is not None:
+            ev1.record()
+            nbytes = 4 * (x.numel() + y.numel() * (2 if res is not None else 1) + pool.numel()) + \
+                self.wpack.numel() * self.wpack.element_size()
+            timer.records.append((ev0, ev1, profiling.conv_flops(self.cin, self.cout, self.ksize, 1, False, B, H, W),
+                                  f"conv{self.ksize}s1 {self.cin}->{self.cout} @{H}x{W} x3 +pool", True, nbytes))
+        return y, pool
+
     def tap_fusable(self, tap: "TapConsumer") -> bool:
         """True if this conv can run with ``tap``'s 1x1 partial GEMM fused into its epilogue
         (split-precision path, its output feeds tap's layer, every output channel in one wave)."""

@@ -221,6 +221,16 @@ class ResBlock(nn.Module):
         y = self.conv1.packed()(x, in_op=K.IN_RELU, act=K.ACT_RELU)
         return self.conv2.packed()(y, res=x)
 
+    def run_pool(self, x):
+        """(out, avg_pool2d(out, 2)): the pool (endecoder.py:272,274) comes out of conv2's epilogue
+        on the split-precision path (FVC_POOL_FUSE=0: separate kernel)."""
+        y = self.conv1.packed()(x, in_op=K.IN_RELU, act=K.ACT_RELU)
+        p = self.conv2.packed()
+        if os.environ.get("FVC_POOL_FUSE", "1") != "0" and p.pool_fusable():
+            return p.call_pool(y, res=x)
+        out = p(y, res=x)
+        return out, K.avgpool2(out)
+
 
 class Warp_net(nn.Module):
     """endecoder.py:262-296."""
@@ -234,9 +244,9 @@ class Warp_net(nn.Module):
 
     def run(self, x8, warpframe):
         fe = self.feature_ext.packed()(x8, act=K.ACT_RELU)
-        c0 = self.conv0.run(fe)
-        c1 = self.conv1.run(K.avgpool2(c0))
-        c2 = self.conv2.run(K.avgpool2(c1))
+        c0, p0 = self.conv0.run_pool(fe)
+        c1, p1 = self.conv1.run_pool(p0)
+        c2 = self.conv2.run(p1)
         c3 = self.conv3.run(c2)
         c3u = K.upsample2x_add(c3, skip=c1, align_corners=True)
         c4 = self.conv4.run(c3u)

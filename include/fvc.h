@@ -120,6 +120,14 @@ int fvc_conv2d_nhwc_x3_tap(const float* x, const void* wpack, float osc, const f
                            int ksize, int stride, int act, const void* tap_wpack, float tap_osc,
                            int pcp, int cu_reserve, int* overflow_flag, int* sched, int sched_len,
                            fvc_stream_t stream);
+/* y = fvc_conv2d_nhwc_x3(x, stride 1, in_op none, post none) and pool = avg_pool2d(y, 2)
+ * [batch][h/2][w/2][cp] in the same launch (Warp_net's ResBlock output feeding F.avg_pool2d,
+ * endecoder.py:272,274; bit-identical to fvc_avgpool2_nhwc of y). */
+int fvc_conv_x3_pool_supported(int cin, int cout, int ksize);
+int fvc_conv2d_nhwc_x3_pool(const float* x, const void* wpack, float osc, const float* bias,
+                            const float* res, float* y, float* pool, int batch, int h, int w, int cin,
+                            int cout, int ksize, int act, int cu_reserve, int* overflow_flag, int* sched,
+                            int sched_len, fvc_stream_t stream);
 int fvc_deconv2d_nhwc_x3_tap(const float* x, const void* wpack, float osc, const float* bias,
                              const float* res, float* P, int batch, int h, int w, int cin, int cout,
                              int ksize, int stride, int act, const void* tap_wpack, float tap_osc,

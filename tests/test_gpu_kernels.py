@@ -202,6 +202,34 @@ def test_conv_then_tap_fused(dev, case, monkeypatch):
     close(from_nhwc(out2.cpu(), c2), from_nhwc(oc, c2), 2e-6)
 
 
+@pytest.mark.parametrize("shape", [(2, 64, 64, 38, 70), (1, 64, 64, 33, 45), (3, 32, 64, 16, 32), (2, 64, 32, 20, 96)])
+@pytest.mark.parametrize("with_res", [False, True])
+def test_conv_x3_pool_epilogue(dev, shape, with_res, monkeypatch):
+    """Conv with avg_pool2d(y, 2) in its epilogue (fvc_conv2d_nhwc_x3_pool): y identical to the
+    plain launch, the pool identical (bits) to fvc_avgpool2_nhwc of y, odd sizes floored; also
+    through the batch split (FVC_X3_SPLIT_BYTES)."""
+    B, ci, co, H, W = shape
+    g = torch.Generator().manual_seed(B + ci + H)
+    x = to_nhwc(torch.randn(B, ci, H, W, generator=g)).to(dev)
+    w = torch.randn(co, ci, 3, 3, generator=g) * (1.0 / (ci * 9) ** 0.5)
+    b = torch.randn(co, generator=g) * 0.1
+    res = to_nhwc(torch.randn(B, co, H, W, generator=g)).to(dev) if with_res else None
+    pc = K.PackedConv(w, b, 3, 1, False, dev, precision="x3")
+    assert pc.pool_fusable()
+    y0 = pc(x, act=K.ACT_RELU, res=res)
+    p0 = K.avgpool2(y0[:, :H // 2 * 2, :W // 2 * 2].contiguous())  # avg_pool2d floors odd sizes
+    y1, p1 = pc.call_pool(x, act=K.ACT_RELU, res=res)
+    torch.cuda.synchronize()
+    assert torch.equal(y0, y1)
+    assert p1.shape == (B, H // 2, W // 2, K.cp4(co))
+    assert torch.equal(p0, p1)
+    if B > 1:
+        monkeypatch.setenv("FVC_X3_SPLIT_BYTES", str(H * W * K.cp4(co) * 4 + 4))  # one image per launch
+        y2, p2 = pc.call_pool(x, act=K.ACT_RELU, res=res)
+        torch.cuda.synchronize()
+        assert torch.equal(y0, y2) and torch.equal(p0, p2)
+
+
 @pytest.mark.parametrize("wn", ["1", "2", "4"])
 def test_conv_x3_ntile_groupings(dev, wn, monkeypatch):
     """The stride-2 128->128 conv with 1, 2 or all 4 N-tiles per block (FVC_X3_WN; 4 is the
