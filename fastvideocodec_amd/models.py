@@ -72,10 +72,16 @@ def get_DVC_pretrained(level, checkpoint=None, seed=20261015, device=None):
 
 def get_codec_model(name, loss_type="P", compression_level=2, noMeasure=True, use_split=True, num_views=0,
                     resilience=0, use_attn=True, load_with_copy=False, **kw):
-    """models.py:32-66 — only the DVC-pretrained codec is built here."""
+    """models.py:32-66 — the codecs this build implements: 'DVC-pretrained' (the hot path) and
+    'RLVC' (IterPredVideoCodecs, models.py:954-1051, eval forward: rlvc.py)."""
     if name in ["DVC-pretrained"]:
         return get_DVC_pretrained(compression_level, **kw)
-    raise NotImplementedError(f"codec {name!r} is outside this build's scope (DVC-pretrained only)")
+    if name == "RLVC":
+        from .rlvc import get_rlvc_model
+        m = get_rlvc_model(**kw)
+        m.name, m.loss_type, m.compression_level = name, loss_type, compression_level
+        return m
+    raise NotImplementedError(f"codec {name!r} is outside this build's scope (DVC-pretrained, RLVC)")
 
 
 class AverageMeter(object):

@@ -61,7 +61,9 @@ def test_models_api_surface():
     with pytest.raises(ValueError):  # no CPU fallback: the product path is HIP-only
         m(x, x)
     with pytest.raises(NotImplementedError):
-        get_codec_model("RLVC")
+        get_codec_model("ELFVC")
+    r = get_codec_model("RLVC", compression_level=2, device="cpu")  # models.py:33 IterPredVideoCodecs
+    assert (r.name, r.compression_level, r.loss_type) == ("RLVC", 2, "P")
 
 
 def test_state_dict_matches_reference_layout():
