@@ -5,6 +5,7 @@
 // contraction off (no FMA fusion) and in the reference's operand order, so results track the
 // CPU path to ~1 ulp.
 #include "fvc_common.h"
+#include <stdlib.h>
 #include "fvc_dist.h"
 #include <string.h>
 
@@ -99,18 +100,19 @@ __global__ __launch_bounds__(256) void k_tap_gather(const float* __restrict__ P,
 // stages the P tile of its 16 x 32 outputs plus a 1-pixel halo with coalesced 16-B loads (zeros
 // outside the image), pixel stride pcp + 1 words so the per-tap reads of consecutive outputs hit
 // distinct banks, then sums bias + taps in k_tap_gather's order (an out-of-image tap adds +0).
-template <int COUT>
+template <int COUT, int TH>
 __global__ __launch_bounds__(256) void k_tap_gather3_lds(const float* __restrict__ P, int pcp,
                                                          const float* __restrict__ bias,
                                                          const float* __restrict__ res, float* __restrict__ y,
                                                          int H, int W, float act_slope, int post_op) {
-  constexpr int TH = 16, TW = 32, IR = TH + 2, IC = TW + 2;
+  constexpr int TW = 32, IR = TH + 2, IC = TW + 2;
   extern __shared__ float sp[];
   const int ps = pcp + 1;
   const int c4n = pcp >> 2;
   const size_t b = blockIdx.z;
   const int y0 = blockIdx.y * TH, x0 = blockIdx.x * TW;
   const float* Pb = P + b * H * W * pcp;
+#pragma unroll 4
   for (int e = threadIdx.x; e < IR * IC * c4n; e += blockDim.x) {
     const int c4 = e % c4n, p = e / c4n;
     const int iy = y0 - 1 + p / IC, ix = x0 - 1 + p % IC;
@@ -862,18 +864,22 @@ int fvc_tap_gather_nhwc(const float* P, int pcp, const float* bias, const float*
   const dim3 g(grid_for(n)), bl(kBlk);
   hipStream_t st = (hipStream_t)s;
   if (!transposed && ksize == 3 && pcp <= 32) {
-    const dim3 gt(fvc_cdiv(w, 32), fvc_cdiv(h, 16), batch);
-    const size_t lds = (size_t)18 * 34 * (pcp + 1) * 4;
-#define FVC_TGL(CO)                                                                                             \
-    if (cout == CO) {                                                                                         \
+    // 8-row tiles: 39 KB of LDS at pcp 28, four blocks per CU (FVC_GATHER_TH=16: 18-row halo tiles)
+    const char* th_env = getenv("FVC_GATHER_TH");
+    const int th = (th_env && atoi(th_env) == 16) ? 16 : 8;
+    const dim3 gt(fvc_cdiv(w, 32), fvc_cdiv(h, th), batch);
+    const size_t lds = (size_t)(th + 2) * 34 * (pcp + 1) * 4;
+#define FVC_TGL(CO, TH)                                                                                         \
+    if (cout == CO && th == TH) {                                                                             \
       if (lds > 64 * 1024)                                                                                    \
-        (void)hipFuncSetAttribute((const void*)k_tap_gather3_lds<CO>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+        (void)hipFuncSetAttribute((const void*)k_tap_gather3_lds<CO, TH>, hipFuncAttributeMaxDynamicSharedMemorySize, \
                                   (int)lds);                                                                  \
-      hipLaunchKernelGGL((k_tap_gather3_lds<CO>), gt, dim3(256), lds, st, P, pcp, bias, res, y, h, w, slope, post_op); \
+      hipLaunchKernelGGL((k_tap_gather3_lds<CO, TH>), gt, dim3(256), lds, st, P, pcp, bias, res, y, h, w, slope, post_op); \
       FVC_CHECK_LAUNCH();                                                                                     \
       return 0;                                                                                               \
     }
-    FVC_TGL(1) FVC_TGL(2) FVC_TGL(3) FVC_TGL(4)
+    FVC_TGL(1, 8) FVC_TGL(2, 8) FVC_TGL(3, 8) FVC_TGL(4, 8)
+    FVC_TGL(1, 16) FVC_TGL(2, 16) FVC_TGL(3, 16) FVC_TGL(4, 16)
 #undef FVC_TGL
   }
   if (transposed && pcp <= 128) {
