@@ -1,0 +1,67 @@
+"""BASELINE.json configs exercised through the bench's own per-rank job on one GPU (small frames,
+so the checks run in seconds): configs[4] (8 camera views, one GOP stream per view, view v on rank
+v % world) and the default GOP sharding. The properties are size-independent: decoder recon ==
+encoder recon bit for bit, every view coded in the batch == that view coded alone (views are
+independent streams), and the rank job's verify() agrees."""
+import argparse
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _args(**kw):
+    a = argparse.Namespace(gpus=1, steps=1, warmup=0, height=96, width=128, gop=3, gops_per_gpu=2, views=0,
+                           cpu_baseline="none", json_out=None, breakdown=False, tree=False, serial=False)
+    for k, v in kw.items():
+        setattr(a, k, v)
+    return a
+
+
+def test_views_config_one_gpu(dev):
+    """configs[4] on one GPU (bench --views 8): all 8 views batch into one rank's job; each view's
+    decoded frames equal the same view coded alone, and the decoder is bit-exact."""
+    import bench
+    from fastvideocodec_amd.gop import encode_decode_gop
+
+    job = bench.GpuGopJob(_args(views=8), 0, 1, dev)
+    assert job.units == 8 and tuple(job.frames.shape[:2]) == (8, 3)
+    job.step()
+    job.sync()
+    v = job.verify()
+    assert v["bitexact"] and v["nbytes"] > 0 and v["overflow_recomputes"] == 0
+    _, dec_all, _, _ = encode_decode_gop(job.model, job.frames, check=True, overlap=True)
+    for view in (0, 5):
+        _, dec_one, _, enc_one = encode_decode_gop(job.model, job.frames[view:view + 1], check=True, overlap=False)
+        torch.cuda.synchronize()
+        for a, b, c in zip(dec_all, dec_one, enc_one):
+            assert torch.equal(a[view:view + 1], b) and torch.equal(b, c)
+
+
+def test_views_shard_over_ranks_match_one_rank(dev):
+    """configs[4] over 2 ranks (run here one after the other on the same GPU): rank r codes views
+    r, r+2, ...; the union of the two ranks' payloads has the same size as the one-rank run."""
+    import bench
+
+    one = bench.GpuGopJob(_args(views=4), 0, 1, dev)
+    r0 = bench.GpuGopJob(_args(views=4), 0, 2, dev)
+    r1 = bench.GpuGopJob(_args(views=4), 1, 2, dev)
+    assert (one.units, r0.units, r1.units) == (4, 2, 2)
+    np.testing.assert_array_equal(r0.gops_np[1], one.gops_np[2])  # rank 0 holds views 0 and 2
+    np.testing.assert_array_equal(r1.gops_np[0], one.gops_np[1])  # rank 1 holds views 1 and 3
+    v_one, v0, v1 = one.verify(), r0.verify(), r1.verify()
+    assert v_one["bitexact"] and v0["bitexact"] and v1["bitexact"]
+    assert v0["nbytes"] + v1["nbytes"] == v_one["nbytes"]
+
+
+def test_run_rank_default_config(dev):
+    """bench.run_rank on one rank with the real GPU job: the result line carries the headline
+    fields and the decoder bit-exactness check."""
+    import bench
+
+    job = bench.GpuGopJob(_args(steps=2, warmup=1), 0, 1, dev)
+    res = bench.run_rank(job, job.args, 0, 1, dev)
+    assert res["n_gpus"] == 1 and res["steps"] == 2 and res["value"] > 0
+    assert res["quality"]["decoder_bitexact"] is True
