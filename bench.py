@@ -1,7 +1,7 @@
 """1080p DVC P-frame encode+decode throughput on MI355X (BASELINE.json metric, configs[2]).
 
-A step = G GOP-12s per GPU batched along dim 0 (G = --gops-per-gpu, default 4; default 2 timed
-steps = 8 GOPs per run), one GOP per batch slot, at 1920x1080
+A step = G GOP-12s per GPU batched along dim 0 (G = --gops-per-gpu, default 8; default 2 timed
+steps = 16 GOPs per run), one GOP per batch slot, at 1920x1080
 (replicate-padded to 1920x1088): frame 0 is the I-frame (passed through; BPG is out of scope),
 frames 1..11 are DVC P-frames, each encoded (full encoder forward incl. its reconstruction, then
 rANS range coding of mv / z / feature into a bitstream) and decoded (rANS decode -> hyperprior ->
@@ -433,9 +433,10 @@ def parse_args(argv=None):
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--gop", type=int, default=12)
-    ap.add_argument("--gops-per-gpu", type=int, default=4,
-                    help="GOPs batched per rank per step (SURVEY §8(e)); default 4 x 2 steps = 8 GOPs per run "
-                         "(§8(d)). Measured on MI355X: 1 -> 44.5, 2 -> 47.6, 4 -> 49.1 P-frames/s")
+    ap.add_argument("--gops-per-gpu", type=int, default=8,
+                    help="GOPs batched per rank per step (SURVEY §8(e)); default 8 x 2 steps = 16 GOPs per run "
+                         "(§8(d)). Measured on MI355X (r2, fused epilogues, 3 steps): 4 -> 56.1/56.2, "
+                         "6 -> 56.9, 8 -> 58.2/58.9/58.7, 12 -> 58.8, 16 -> 59.3 P-frames/s")
     ap.add_argument("--views", type=int, default=0,
                     help="BASELINE configs[4]: V camera views, one GOP stream each, view v -> rank v %% world "
                          "(replaces --gops-per-gpu; the reference's MCVC couples views, DVC views are independent)")
