@@ -27,6 +27,7 @@
 namespace {
 
 constexpr int kMaxTaps = 49;
+typedef float f2v __attribute__((ext_vector_type(2)));
 constexpr int kThreads = 256;
 
 struct ConvArgs {
@@ -157,23 +158,26 @@ __global__ __launch_bounds__(kThreads) void conv_mfma_f32_kernel(const ConvArgs 
       } else {
         if (q + 1 < nq) loadB(q + 1, Bn);
       }
-      // element-major issue order: consecutive MFMAs hit different accumulators (no RAW chain)
+      // element-major issue order: consecutive MFMAs hit different accumulators (no RAW chain).
+      // Weights are the row operand and pixels the column operand, so each lane ends with 4
+      // consecutive channels of one pixel per register group (16-B epilogue stores); the two
+      // products of each MFMA and their order are the same either way.
 #pragma unroll
       for (int m = 0; m < WM; ++m)
 #pragma unroll
-        for (int n = 0; n < WN; ++n) acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x2f32(A[m].x, Bv[n].x, acc[m][n], 0, 0, 0);
+        for (int n = 0; n < WN; ++n) acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x2f32(Bv[n].x, A[m].x, acc[m][n], 0, 0, 0);
 #pragma unroll
       for (int m = 0; m < WM; ++m)
 #pragma unroll
-        for (int n = 0; n < WN; ++n) acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x2f32(A[m].y, Bv[n].y, acc[m][n], 0, 0, 0);
+        for (int n = 0; n < WN; ++n) acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x2f32(Bv[n].y, A[m].y, acc[m][n], 0, 0, 0);
 #pragma unroll
       for (int m = 0; m < WM; ++m)
 #pragma unroll
-        for (int n = 0; n < WN; ++n) acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x2f32(A[m].z, Bv[n].z, acc[m][n], 0, 0, 0);
+        for (int n = 0; n < WN; ++n) acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x2f32(Bv[n].z, A[m].z, acc[m][n], 0, 0, 0);
 #pragma unroll
       for (int m = 0; m < WM; ++m)
 #pragma unroll
-        for (int n = 0; n < WN; ++n) acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x2f32(A[m].w, Bv[n].w, acc[m][n], 0, 0, 0);
+        for (int n = 0; n < WN; ++n) acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x2f32(Bv[n].w, A[m].w, acc[m][n], 0, 0, 0);
 #pragma unroll
       for (int m = 0; m < WM; ++m) A[m] = An[m];
 #pragma unroll
@@ -185,34 +189,40 @@ __global__ __launch_bounds__(kThreads) void conv_mfma_f32_kernel(const ConvArgs 
     __syncthreads();
   }
 
-  // ---- epilogue
+  // ---- epilogue: lane (li, lh) holds pixel qx0 + li; register group g holds output channels
+  // N-tile*32 + 8g + 4lh + {0..3} -> one 16-B store (and residual load) per group
   const int oy0 = a.oy0[cls], ox0 = a.ox0[cls];
+  const int qx = qx0 + li;
+  if (qx >= a.Wq) return;
+  const int ox = qx * a.sout + ox0;
 #pragma unroll
-  for (int n = 0; n < WN; ++n) {
-    const int j = (nt0 + n) * 32 + li;
-    if (j >= a.coutp) continue;
-    const bool real = j < a.cout;
-    const float bj = real ? a.bias[j] : 0.f;
+  for (int m = 0; m < WM; ++m) {
+    const int qy = qy0 + wave * WM + m;
+    if (qy >= a.Hq) continue;
+    const int oy = qy * a.sout + oy0;
+    const size_t obase = (((size_t)b * a.Ho + oy) * a.Wo + ox) * a.coutp;
 #pragma unroll
-    for (int m = 0; m < WM; ++m) {
-      const int qy = qy0 + wave * WM + m;
-      if (qy >= a.Hq) continue;
-      const int oy = qy * a.sout + oy0;
+    for (int n = 0; n < WN; ++n)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int pi = (r & 3) + 8 * (r >> 2) + 4 * lh;
-        const int qx = qx0 + pi;
-        if (qx >= a.Wq) continue;
-        const int ox = qx * a.sout + ox0;
-        const size_t o = (((size_t)b * a.Ho + oy) * a.Wo + ox) * a.coutp + j;
-        float v = acc[m][n][r] + bj;
-        if (a.act == FVC_ACT_RELU) v = v > 0.f ? v : 0.f;
-        else if (a.act == FVC_ACT_LRELU) v = v > 0.f ? v : 0.1f * v;
-        if (a.res) v += a.res[o];
-        if (a.post_op == FVC_POST_EXP) v = expf(v);
-        a.y[o] = real ? v : 0.f;
+      for (int g = 0; g < 4; ++g) {
+        const int j0 = (nt0 + n) * 32 + 8 * g + 4 * lh;
+        if (j0 >= a.coutp) continue;  // coutp is a multiple of 4: whole groups
+        float4 rv = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (a.res) rv = *reinterpret_cast<const float4*>(a.res + obase + j0);
+        const float rr[4] = {rv.x, rv.y, rv.z, rv.w};
+        float o[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const bool real = j0 + i < a.cout;
+          float v = acc[m][n][4 * g + i] + (real ? a.bias[j0 + i] : 0.f);
+          if (a.act == FVC_ACT_RELU) v = v > 0.f ? v : 0.f;
+          else if (a.act == FVC_ACT_LRELU) v = v > 0.f ? v : 0.1f * v;
+          if (a.res) v += rr[i];
+          if (a.post_op == FVC_POST_EXP) v = expf(v);
+          o[i] = real ? v : 0.f;
+        }
+        *reinterpret_cast<float4*>(a.y + obase + j0) = make_float4(o[0], o[1], o[2], o[3]);
       }
-    }
   }
 }
 
@@ -629,8 +639,21 @@ __global__ __launch_bounds__(kThreads) void conv_smalln_f32_kernel(const ConvArg
             for (int k = 0; k < PY; ++k) {
               const float4 xv = v[k + dyi];
               const float xs = e == 0 ? xv.x : (e == 1 ? xv.y : (e == 2 ? xv.z : xv.w));
+              if constexpr (COUT % 2 == 0) {
+                // channel pairs as one packed FMA (v_pk_fma_f32): the same fp32 fma per channel
 #pragma unroll
-              for (int j = 0; j < COUT; ++j) acc[k][j] = __builtin_fmaf(xs, wv[e * COUT + j], acc[k][j]);
+                for (int j = 0; j < COUT; j += 2) {
+                  const f2v xx = {xs, xs};
+                  const f2v ww = {wv[e * COUT + j], wv[e * COUT + j + 1]};
+                  const f2v aa = {acc[k][j], acc[k][j + 1]};
+                  const f2v rr = __builtin_elementwise_fma(xx, ww, aa);
+                  acc[k][j] = rr[0];
+                  acc[k][j + 1] = rr[1];
+                }
+              } else {
+#pragma unroll
+                for (int j = 0; j < COUT; ++j) acc[k][j] = __builtin_fmaf(xs, wv[e * COUT + j], acc[k][j]);
+              }
             }
         }
       }
