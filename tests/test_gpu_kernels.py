@@ -343,13 +343,20 @@ def test_warp(dev):
 
 
 @pytest.mark.parametrize("ac", [False, True])
-def test_upsample_add(dev, ac):
+@pytest.mark.parametrize("scale", [1.0, 2.0])
+def test_upsample_add(dev, ac, scale):
+    """64 channels at scale 1 take the 32-bit two-quads-per-thread path (k_up2_add_c16), the rest
+    the generic kernel; both against the oracle's upsample, and the fast path bit-identical to
+    the generic one on the same data (68 channels = 64 + 4 zero pad channels go generic)."""
     g = torch.Generator().manual_seed(2)
     src = torch.randn(2, 64, 9, 15, generator=g)
     skip = torch.randn(2, 64, 18, 30, generator=g)
-    ref = skip + dvc_ref.up2(src, ac) * (1.0 if ac else 2.0)
-    y = K.upsample2x_add(to_nhwc(src).to(dev), to_nhwc(skip).to(dev), align_corners=ac, scale=1.0 if ac else 2.0)
+    ref = skip + dvc_ref.up2(src, ac) * scale
+    y = K.upsample2x_add(to_nhwc(src).to(dev), to_nhwc(skip).to(dev), align_corners=ac, scale=scale)
     close(from_nhwc(y.cpu(), 64), ref, 1e-6)
+    y68 = K.upsample2x_add(to_nhwc(src, 68).to(dev), to_nhwc(skip, 68).to(dev), align_corners=ac, scale=scale)
+    torch.cuda.synchronize()
+    assert torch.equal(y68[..., :64], y)
 
 
 def test_avgpool(dev):
