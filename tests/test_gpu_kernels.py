@@ -345,9 +345,8 @@ def test_warp(dev):
 @pytest.mark.parametrize("ac", [False, True])
 @pytest.mark.parametrize("scale", [1.0, 2.0])
 def test_upsample_add(dev, ac, scale):
-    """64 channels at scale 1 take the 32-bit two-quads-per-thread path (k_up2_add_c16), the rest
-    the generic kernel; both against the oracle's upsample, and the fast path bit-identical to
-    the generic one on the same data (68 channels = 64 + 4 zero pad channels go generic)."""
+    """Against the oracle's upsample (both align_corners modes, scale 1 and SpyNet's 2), and the
+    channel-padded run (68 = 64 + 4 zero pad channels) bit-identical on the real channels."""
     g = torch.Generator().manual_seed(2)
     src = torch.randn(2, 64, 9, 15, generator=g)
     skip = torch.randn(2, 64, 18, 30, generator=g)
