@@ -66,7 +66,7 @@ _SIGS = {
     "fvc_rans_lut_bytes": (c_size_t, [c_int, c_int]),
     "fvc_rans_build_lut": (c_int, [vp, c_int, vp, c_int, vp, vp]),
     "fvc_rans_pack": (c_int, [vp, vp, vp, c_int, vp, vp, vp, vp]),
-    "fvc_rans_decode": (c_int, [vp, vp, vp, vp, c_int, c_int, c_int, vp, vp, vp, vp, vp, vp]),
+    "fvc_rans_decode": (c_int, [vp, vp, vp, vp, c_int, c_int, c_int, vp, vp, vp, vp, vp, c_int, vp]),
     "fvc_iframe_rct_fwd": (c_int, [vp, vp, c_int, c_int, c_int, vp]),
     "fvc_iframe_rct_inv": (c_int, [vp, vp, c_int, c_int, c_int, vp]),
     "fvc_iframe_dwt53": (c_int, [vp, vp, c_int, c_int, c_int, c_int, c_int, vp]),

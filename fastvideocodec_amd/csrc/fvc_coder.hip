@@ -7,6 +7,7 @@
 // Parallelism: one lane per independent stream (a stream = one channel of one latent of one
 // frame); a stream's symbol loop is inherently sequential (rANS state chain).
 #include "fvc_common.h"
+#include <stdlib.h>
 
 namespace {
 
@@ -349,6 +350,7 @@ constexpr int kTabWords = 25600;      // 100 KB of table images
 constexpr size_t kDec2Lds =
     (size_t)(2 * kJ * 64 * 4 + 2 * kJ * 64 + kR * 64 + 3 * 64 + 4 + 2 * kTabDir + kTabWords) * 4;
 constexpr uint32_t kGlobTab = 0x80000000u;  // record flag: table image read from global memory
+constexpr int kDecSpb = 64;                 // streams per decode block when the caller passes 0
 constexpr int kRsrcFlags = 0x00020000;  // buffer descriptor dword 3 (raw 32-bit, as fvc_conv_x3.hip)
 
 // Global reads that sit next to LDS reads of the same value go through buffer descriptors: a
@@ -365,7 +367,7 @@ __global__ __launch_bounds__(128) void k_rans_decode(
     const uint32_t* __restrict__ packed, const int64_t* __restrict__ pack_off, const int32_t* __restrict__ indexes,
     const int64_t* __restrict__ sym_off, int nstreams, const int32_t* __restrict__ cdf_sizes,
     const int32_t* __restrict__ offsets, int ntables, const uint32_t* __restrict__ img_off, const uint32_t* __restrict__ img,
-    int32_t* __restrict__ symbols, int32_t* __restrict__ status) {
+    int32_t* __restrict__ symbols, int32_t* __restrict__ status, int spb) {
   extern __shared__ int32_t lds[];
   uint4* const s_rec = reinterpret_cast<uint4*>(lds);          // [2][kJ][64] {ci, off, tab, -}
   int32_t* const s_out = lds + 2 * kJ * 64 * 4;                // [2][kJ][64] decoded symbols
@@ -378,8 +380,10 @@ __global__ __launch_bounds__(128) void k_rans_decode(
   uint32_t* const s_tab = (uint32_t*)(s_doff + kTabDir);       // [kTabWords] table images
   const int lane = threadIdx.x & 63;
   const bool loader = threadIdx.x >= 64;
-  const int s = blockIdx.x * 64 + lane;
-  const bool live = s < nstreams;
+  // spb streams per block (lanes >= spb idle): with fewer streams a block's table cache holds the
+  // tables of all of them, so no lane of the decoder wave waits on L2 per symbol
+  const int s = blockIdx.x * spb + lane;
+  const bool live = lane < spb && s < nstreams;
   const int64_t w0 = live ? pack_off[s] : 0;
   const int nw = live ? (int)(pack_off[s + 1] - w0) : 0;
   const int64_t b = live ? sym_off[s] : 0;
@@ -723,15 +727,17 @@ int fvc_rans_pack(const uint32_t* words, const int64_t* word_off, const int32_t*
 
 int fvc_rans_decode(const uint32_t* packed, const int64_t* pack_off, const int32_t* indexes, const int64_t* sym_off,
                     int nstreams, int ntables, int cdf_stride, const int32_t* cdf_sizes, const int32_t* offsets,
-                    const void* lut, int32_t* symbols, int32_t* status, fvc_stream_t s) {
+                    const void* lut, int32_t* symbols, int32_t* status, int streams_per_block, fvc_stream_t s) {
   if (!packed || !pack_off || !indexes || !sym_off || !cdf_sizes || !offsets || !lut || !symbols || !status ||
       nstreams <= 0 || ntables <= 0 || cdf_stride <= 1)
     return FVC_EINVAL;
   const uint32_t* img_off = (const uint32_t*)lut;
   (void)hipFuncSetAttribute((const void*)k_rans_decode, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kDec2Lds);
-  hipLaunchKernelGGL(k_rans_decode, dim3((nstreams + 63) / 64), dim3(128), kDec2Lds, (hipStream_t)s, packed, pack_off,
-                     indexes, sym_off, nstreams, cdf_sizes, offsets, ntables, img_off, img_off + ntables + 1, symbols,
-                     status);
+  if (streams_per_block < 0 || streams_per_block > 64) return FVC_EINVAL;
+  const int spb = streams_per_block ? streams_per_block : kDecSpb;
+  hipLaunchKernelGGL(k_rans_decode, dim3((nstreams + spb - 1) / spb), dim3(128), kDec2Lds, (hipStream_t)s, packed,
+                     pack_off, indexes, sym_off, nstreams, cdf_sizes, offsets, ntables, img_off, img_off + ntables + 1,
+                     symbols, status, spb);
   FVC_CHECK_LAUNCH();
   return 0;
 }

@@ -244,7 +244,8 @@ class RangeCoder:
         _lib.call("fvc_rans_decode", enc.packed.data_ptr(), enc.pack_off.data_ptr(), indexes.data_ptr(),
                   sym_off.data_ptr(), S, self.ntables, self.cdf.shape[1], self.cdf_length.data_ptr(),
                   self.offset.data_ptr(),
-                  self.lut.data_ptr(), out.data_ptr(), status.data_ptr(), K.stream_handle())
+                  self.lut.data_ptr(), out.data_ptr(), status.data_ptr(), K.rans_streams_per_block(),
+                  K.stream_handle())
         if check and int(status.abs().max()) != 0:
             raise _lib.FvcError("corrupt rANS stream")
         return out

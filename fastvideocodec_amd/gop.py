@@ -129,7 +129,7 @@ def _encode_decode_gop(model, frames, check, overlap, join):
     bitstreams, decoded, sses, enc_recons, keep = [], [], [], [], [x_enc]
     model.update()
     # launches outside the pipeline get the whole GPU: the reserve applies inside this block only
-    with torch.no_grad(), K.cu_reserve(PIPELINE_CU_RESERVE if overlap else 0):
+    with torch.no_grad(), K.cu_reserve(PIPELINE_CU_RESERVE if overlap else 0), K.rans_throughput(overlap):
         for t in range(1, T):
             cur = frames[:, t].contiguous()
             tens = model._encode_graph(cur, x_enc)

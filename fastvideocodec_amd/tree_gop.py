@@ -134,7 +134,7 @@ def _tree(model, frames, check, overlap, isLinear, isOnehop, probes):
     model.update()
     if K.conv_precision() != "f32":
         K.overflow_flag(frames.device).zero_()
-    with torch.no_grad(), K.cu_reserve(PIPELINE_CU_RESERVE if overlap else 0):
+    with torch.no_grad(), K.cu_reserve(PIPELINE_CU_RESERVE if overlap else 0), K.rans_throughput(overlap):
         for i, layer in enumerate(lay):
             cur = torch.cat([frames[:, t] for t, _ in layer], 0).contiguous()
             ref_e = torch.cat([enc[p] for _, p in layer], 0).contiguous()

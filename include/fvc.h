@@ -247,10 +247,14 @@ int fvc_rans_build_lut(const int32_t* cdfs, int cdf_stride, const int32_t* cdf_s
                        void* lut, fvc_stream_t stream);
 /* Decode: stream s reads packed words starting at pack_off[s]; status[s] = 0 or FVC_ECORRUPT.
  * Output identical to compressai RansDecoder.decode_with_indexes per stream. */
+/* streams_per_block (1..64, 0 = 64): a block decodes that many streams, one lane each. Fewer
+ * streams per block keep every stream's tables in the block's LDS cache (no lane waits on L2 per
+ * symbol: lower latency), more leave CUs free for concurrent kernels (higher pipelined throughput):
+ * the GOP pipeline passes 64, latency-bound decodes 16. */
 int fvc_rans_decode(const uint32_t* packed, const int64_t* pack_off, const int32_t* indexes,
                     const int64_t* sym_off, int nstreams, int ntables, int cdf_stride,
                     const int32_t* cdf_sizes, const int32_t* offsets, const void* lut,
-                    int32_t* symbols, int32_t* status, fvc_stream_t stream);
+                    int32_t* symbols, int32_t* status, int streams_per_block, fvc_stream_t stream);
 
 /* ------------------------------------------------------------------ I-frame codec
  * Replaces the reference's BPG I-frame (models.py:412-429 I_compression: bpgenc/bpgdec through

@@ -464,6 +464,23 @@ def test_rans_device_vs_oracle(dev):
         assert (dec == sym).all()
 
 
+@pytest.mark.parametrize("spb", [1, 7, 16, 64])
+def test_rans_decode_streams_per_block(dev, spb, monkeypatch):
+    """fvc_rans_decode with 1..64 streams per block (ragged last block) decodes the same symbols;
+    the pipeline's throughput setting (64) and the latency default (16) included."""
+    rng = np.random.default_rng(40 + spb)
+    lt = EM.LaplaceTables()
+    coder = EM.RangeCoder(lt.cdf, lt.cdf_length, lt.offset, dev)
+    sym, idx = _rand_streams(45, 700, 64, rng)
+    enc = coder.encode(torch.from_numpy(sym).to(dev), torch.from_numpy(idx).to(dev))
+    monkeypatch.setitem(K._STATE, "rans_spb", spb)
+    dec = coder.decode(enc, torch.from_numpy(idx).to(dev)).cpu().numpy()
+    assert (dec == sym).all()
+    with K.rans_throughput():
+        assert K.rans_streams_per_block() == 64
+    assert K.rans_streams_per_block() == spb
+
+
 def test_rans_compressai_api(dev):
     rng = np.random.default_rng(12)
     ft_prm = rng.normal(0, 0.01, (11, 8)).astype(np.float32)
