@@ -106,6 +106,43 @@ def test_x3_pack_splits_every_weight_once(geom):
     assert 2 ** 13 <= scaled < 2 ** 14
 
 
+@pytest.mark.parametrize("np_cin", [(18, 128), (27, 64), (32, 32), (5, 60)])
+def test_x3_tap_pack_layout(np_cin):
+    """Fused tap epilogue weights (fvc_x3_tap_pack_weight): block kb, lane (li, lh), element t
+    holds row li and channel 16 kb + 4 lh + {0,1,2,3,8,9,10,11}[t] -- the producing tile's
+    accumulator order -- as a hi / lo*2^11 fp16 pair of w*2^kt; rows >= np and channels >= cin
+    are zero. Also the C-ABI support predicate for the two fused pairs and the refusals."""
+    import ctypes
+    lib = _lib.load()
+    npart, cin = np_cin
+    nbytes = lib.fvc_x3_tap_wpack_bytes(npart, cin)
+    nkb = 2 * -(-((cin + 3) // 4 * 4) // 32)  # two k16 blocks per 32-channel N-tile of the producer
+    assert nbytes == nkb * 2 * 64 * 16
+    g = torch.Generator().manual_seed(npart * cin)
+    w = torch.randn(npart, cin, generator=g) * 0.05
+    out = torch.empty(nbytes // 2, dtype=torch.float16)
+    osc = ctypes.c_float(0)
+    assert lib.fvc_x3_tap_pack_weight(w.data_ptr(), out.data_ptr(), ctypes.addressof(osc), npart, cin) == 0
+    fr = out.view(nkb, 2, 64, 8).double()
+    val = (fr[:, 0] + fr[:, 1] * 2.0 ** -11) * osc.value          # [kb][lane][t]
+    perm = [0, 1, 2, 3, 8, 9, 10, 11]
+    expect = torch.zeros(nkb, 64, 8, dtype=torch.float64)
+    for kb in range(nkb):
+        for lane in range(64):
+            li, lh = lane & 31, lane >> 5
+            for t in range(8):
+                ci = 16 * kb + 4 * lh + perm[t]
+                if li < npart and ci < cin:
+                    expect[kb, lane, t] = float(w[li, ci])
+    assert torch.allclose(val, expect, rtol=2 ** -20, atol=float(w.abs().max()) * 2 ** -32)
+    assert lib.fvc_x3_tap_wpack_bytes(33, cin) == 0  # more partials than one P tile
+    assert lib.fvc_conv_x3_tap_supported(128, 128, 3, 2, 1, 20) == 1  # mvDecoder deconv7 -> deconv8
+    assert lib.fvc_conv_x3_tap_supported(64, 64, 3, 1, 0, 28) == 1    # Warp_net conv5 -> conv6
+    assert lib.fvc_conv_x3_tap_supported(64, 64, 3, 1, 0, 30) == 0    # P channels must be a multiple of 4
+    assert lib.fvc_conv_x3_pool_supported(64, 64, 3) == 1
+    assert lib.fvc_conv_x3_pool_supported(128, 128, 3) == 0           # two N-groups: pool needs one wave per pixel
+
+
 def test_x3_rejects_unsupported_layers():
     lib = _lib.load()
     assert lib.fvc_conv_x3_supported(2, 128, 3, 2, 0) == 0  # cin padded to 4: fp32 kernel
