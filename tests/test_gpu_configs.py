@@ -65,3 +65,22 @@ def test_run_rank_default_config(dev):
     res = bench.run_rank(job, job.args, 0, 1, dev)
     assert res["n_gpus"] == 1 and res["steps"] == 2 and res["value"] > 0
     assert res["quality"]["decoder_bitexact"] is True
+
+
+def test_4k_gop_batch_split_pipeline(dev):
+    """configs[3] shape on one GPU: three 4K GOPs (3840x2160 -> 2176) through the overlapped GOP
+    pipeline. Their 64-channel full-resolution activations are 6.4 GB per launch, so every such
+    conv runs as launches over sub-batches (the 32-bit buffer-offset split); the decoder must still
+    match the encoder bit for bit and each GOP must equal that GOP coded alone."""
+    from fastvideocodec_amd.gop import encode_decode_gop
+    from fastvideocodec_amd.models import get_codec_model
+    from fastvideocodec_amd.synthetic import gop_seed, make_gop
+
+    model = get_codec_model("DVC-pretrained", compression_level=2, device=dev)
+    frames = torch.from_numpy(np.stack([make_gop(2160, 3840, 2, gop_seed(g)) for g in (3, 4, 5)])).to(dev)
+    assert 3 * 2176 * 3840 * 64 * 4 >= (1 << 32) - 4096  # the split path is taken
+    _, dec, _, enc = encode_decode_gop(model, frames, check=True, overlap=True)
+    _, dec1, _, enc1 = encode_decode_gop(model, frames[1:2], check=True, overlap=False)
+    torch.cuda.synchronize()
+    for a, b, c in zip(dec, enc, dec1):
+        assert torch.equal(a, b) and torch.equal(a[1:2], c)
