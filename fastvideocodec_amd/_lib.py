@@ -49,6 +49,7 @@ _SIGS = {
     "fvc_tap_gather_nhwc": (c_int, [vp, c_int, vp, vp, vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                                     c_int, c_int, vp]),
     "fvc_gdn_nhwc": (c_int, [vp, vp, vp, vp, c_int, c_int, c_int, c_int, c_int, vp]),
+    "fvc_gdn_tap_nhwc": (c_int, [vp, vp, vp, vp, vp, vp] + [c_int] * 7 + [vp, vp]),
     "fvc_reduce_ws_doubles": (c_size_t, []),
     "fvc_recon_finalize": (c_int, [vp] * 7 + [c_int, c_int, c_int, vp]),
     "fvc_bits_laplace": (c_int, [vp] * 4 + [c_int] * 5 + [vp]),

@@ -499,6 +499,121 @@ __global__ __launch_bounds__(64 * kGdnWaves) void k_gdn_mfma(const float* __rest
   }
 }
 
+// GDN / IGDN followed by the next layer's 1x1 tap-partial GEMM (resDecoder igdn3 -> deconv4,
+// synthesis.py:26,57: 64 -> 3, 5x5 s2, 75 partials): per 32-pixel group the normalised y goes back
+// into the wave's LDS tile (pixel-major), each lane then reads its pixel's channels as split-
+// precision B fragments (channel order of fvc_x3_tap_pack_weight) and NPT P tiles of 32 partials
+// come out of three fp16 MFMAs per k16 block, P = main * 2^-kt + corr * 2^-kt-11. y itself never
+// reaches HBM; fvc_tap_gather_nhwc sums the partials into the deconv's output.
+typedef _Float16 gh8 __attribute__((ext_vector_type(8)));
+template <int NPT>
+__global__ __launch_bounds__(64 * kGdnWaves) void k_gdn_tap_mfma(const float* __restrict__ x, float* __restrict__ P,
+                                                             const float* __restrict__ beta,
+                                                             const float* __restrict__ gamma,
+                                                             const uint4* __restrict__ tw, float4 tosc,
+                                                             size_t npix, int inverse, int pcp, int* ovf) {
+  __shared__ float xt[kGdnWaves * 32 * kGdnRow];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int li = lane & 31, lh = lane >> 5;
+  float g0[32], g1[32];
+#pragma unroll
+  for (int s = 0; s < 32; ++s) {
+    g0[s] = gamma[li * 64 + s + 32 * lh];
+    g1[s] = gamma[(32 + li) * 64 + s + 32 * lh];
+  }
+  const float b0 = beta[li], b1 = beta[32 + li];
+  const float ts[4] = {tosc.x, tosc.y, tosc.z, tosc.w};
+  float* xw = xt + wave * 32 * kGdnRow;
+  const size_t ngroups = (npix + 31) / 32;
+  float4 nx[8];
+  auto fetch = [&](size_t gi) {
+    const size_t p = gi * 32 + li;
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      nx[k] = p < npix ? reinterpret_cast<const float4*>(x + p * 64 + 32 * lh)[k] : make_float4(0.f, 0.f, 0.f, 0.f);
+  };
+  const size_t gstep = (size_t)gridDim.x * kGdnWaves;
+  size_t gi = (size_t)blockIdx.x * kGdnWaves + wave;
+  float mx = 0.f;
+  if (gi < ngroups) fetch(gi);
+  for (; gi < ngroups; gi += gstep) {
+    const size_t p0 = gi * 32;
+    float a[32];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float4 v = nx[k];
+      a[4 * k] = v.x; a[4 * k + 1] = v.y; a[4 * k + 2] = v.z; a[4 * k + 3] = v.w;
+      *reinterpret_cast<float4*>(xw + li * kGdnRow + 32 * lh + 4 * k) = v;
+    }
+    if (gi + gstep < ngroups) fetch(gi + gstep);
+    f32x16 acc0, acc1;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      acc0[r] = 0.f;
+      acc1[r] = 0.f;
+    }
+#pragma unroll
+    for (int s = 0; s < 32; ++s) {
+      const float sq = a[s] * a[s];
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(sq, g0[s], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(sq, g1[s], acc1, 0, 0, 0);
+    }
+    // y (the same expression as k_gdn_mfma) back into the tile; pixels past npix hold 0
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int q = (r & 3) + 8 * (r >> 2) + 4 * lh;
+      const bool ok = p0 + q < npix;
+      const float x0 = xw[q * kGdnRow + li], x1 = xw[q * kGdnRow + 32 + li];
+      const float n0 = sqrtf(acc0[r] + b0), n1 = sqrtf(acc1[r] + b1);
+      const float y0 = inverse ? x0 * n0 : x0 / n0, y1 = inverse ? x1 * n1 : x1 / n1;
+      xw[q * kGdnRow + li] = ok ? y0 : 0.f;
+      xw[q * kGdnRow + 32 + li] = ok ? y1 : 0.f;
+    }
+    // lane (li, lh): pixel li's channels 16 kb + 4 lh + {0-3, 8-11} as hi / lo*2^11 halves
+    gh8 yh[4], yl[4];
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) {
+      const float* row = xw + li * kGdnRow + 16 * kb + 4 * lh;
+      const float4 u = *reinterpret_cast<const float4*>(row), v = *reinterpret_cast<const float4*>(row + 8);
+      const float f[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        const _Float16 h = (_Float16)f[t];
+        yh[kb][t] = h;
+        yl[kb][t] = (_Float16)((f[t] - (float)h) * 2048.f);
+        mx = fmaxf(mx, fabsf(f[t]));
+      }
+    }
+    const bool px_ok = p0 + li < npix;
+#pragma unroll
+    for (int pt = 0; pt < NPT; ++pt) {
+      f32x16 pa, pc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) pa[r] = pc[r] = 0.f;
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb) {
+        const uint4* f = tw + (size_t)((pt * 4 + kb) * 2) * 64 + lane;
+        const gh8 wh = __builtin_bit_cast(gh8, f[0]), wl = __builtin_bit_cast(gh8, f[64]);
+        pa = __builtin_amdgcn_mfma_f32_32x32x16_f16(wh, yh[kb], pa, 0, 0, 0);
+        pc = __builtin_amdgcn_mfma_f32_32x32x16_f16(wl, yh[kb], pc, 0, 0, 0);
+        pc = __builtin_amdgcn_mfma_f32_32x32x16_f16(wh, yl[kb], pc, 0, 0, 0);
+      }
+      const float sc = ts[pt], scc = ts[pt] * (1.0f / 2048.f);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int pp = pt * 32 + 8 * g + 4 * lh;
+        if (px_ok && pp < pcp) {
+          float o[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) o[i] = fmaf(pc[4 * g + i], scc, pa[4 * g + i] * sc);
+          *reinterpret_cast<float4*>(P + (p0 + li) * pcp + pp) = make_float4(o[0], o[1], o[2], o[3]);
+        }
+      }
+    }
+  }
+  if (!(mx < 65000.f) && ovf) atomicOr(ovf, 1);
+}
+
 // ------------------------------------------------------------------ deterministic reductions
 template <int K>
 __device__ void block_reduce_store(double (&v)[K], double* out) {
@@ -987,6 +1102,32 @@ int fvc_gdn_nhwc(const float* x, float* y, const float* beta, const float* gamma
                      npix, inverse);
   FVC_CHECK_LAUNCH();
   return 0;
+}
+
+int fvc_gdn_tap_nhwc(const float* x, float* P, const float* beta, const float* gamma, const void* tap_wpack,
+                     const float* tap_osc, int ntiles, int pcp, int batch, int h, int w, int c, int inverse,
+                     int* overflow_flag, fvc_stream_t s) {
+  if (!x || !P || !beta || !gamma || !tap_wpack || !tap_osc || c != 64 || ntiles < 1 || ntiles > 4 || pcp <= 0 ||
+      pcp % 4 || pcp > 32 * ntiles)
+    return FVC_EINVAL;
+  const size_t npix = (size_t)batch * h * w;
+  size_t nblk = ((npix + 31) / 32 + kGdnWaves - 1) / kGdnWaves;
+  if (nblk > 2048) nblk = 2048;
+  if (nblk < 1) nblk = 1;
+  float t[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int i = 0; i < ntiles; ++i) t[i] = tap_osc[i];
+  const float4 tosc = make_float4(t[0], t[1], t[2], t[3]);
+  const uint4* tw = (const uint4*)tap_wpack;
+#define FVC_GT(N)                                                                                               \
+  if (ntiles == N) {                                                                                          \
+    hipLaunchKernelGGL(k_gdn_tap_mfma<N>, dim3((unsigned)nblk), dim3(64 * kGdnWaves), 0, (hipStream_t)s, x, P, beta, \
+                       gamma, tw, tosc, npix, inverse, pcp, overflow_flag);                                   \
+    FVC_CHECK_LAUNCH();                                                                                       \
+    return 0;                                                                                                 \
+  }
+  FVC_GT(1) FVC_GT(2) FVC_GT(3) FVC_GT(4)
+#undef FVC_GT
+  return FVC_EINVAL;
 }
 
 size_t fvc_reduce_ws_doubles(void) { return (size_t)kRedBlocks * 4; }

@@ -472,6 +472,59 @@ class TapConsumer:
         return y
 
 
+class GdnTap:
+    """GDN / IGDN (64 channels) fused with a cout <= 4 consumer conv / transposed conv in tap form
+    (fvc_gdn_tap_nhwc: up to 4 tiles of 32 partials, so k*k*cout <= 128) + the gather: resDecoder
+    igdn3 -> deconv4 (synthesis.py:26,57; 64 -> 3, 5x5 s2, 75 partials)."""
+
+    def __init__(self, weight: torch.Tensor, bias: torch.Tensor, ksize: int, stride: int, transposed: bool, device):
+        import ctypes
+        lib = _lib.load()
+        w = weight.detach().to("cpu", torch.float32).contiguous()
+        cin, cout = (w.shape[0], w.shape[1]) if transposed else (w.shape[1], w.shape[0])
+        nt = ksize * ksize
+        if cin != 64 or cout > 4 or ksize not in (3, 5) or stride != (2 if transposed else 1) or nt * cout > 128:
+            raise ValueError("GDN + tap form needs 64 input channels, cout <= 4, k 3/5, <= 128 partials")
+        self.cin, self.cout, self.ksize, self.stride, self.transposed = cin, cout, ksize, stride, transposed
+        wt = (w.permute(2, 3, 1, 0) if transposed else w.permute(2, 3, 0, 1)).reshape(nt * cout, cin).contiguous()
+        self.np, self.pcp = nt * cout, cp4(nt * cout)
+        self.ntiles = (self.np + 31) // 32
+        packs, oscs = [], []
+        for t in range(self.ntiles):
+            rows = wt[32 * t: 32 * t + 32].contiguous()
+            nbytes = lib.fvc_x3_tap_wpack_bytes(rows.shape[0], cin)
+            pk = torch.empty(nbytes // 2, dtype=torch.float16)
+            osc = ctypes.c_float(0.0)
+            _lib.call("fvc_x3_tap_pack_weight", rows.data_ptr(), pk.data_ptr(), ctypes.addressof(osc), rows.shape[0], cin)
+            packs.append(pk)
+            oscs.append(float(osc.value))
+        self.wpack = torch.cat(packs).to(device)
+        self.osc = (ctypes.c_float * 4)(*(oscs + [0.0] * (4 - len(oscs))))
+        self.bias = bias.detach().to(device, torch.float32).contiguous()
+
+    def __call__(self, x, beta, gamma, inverse, act=ACT_NONE, post=POST_NONE, res=None):
+        """consumer(gdn(x)) without writing gdn(x)."""
+        import ctypes
+        B, H, W, C = x.shape
+        if C != 64:
+            raise ValueError("GDN + tap needs 64 channels")
+        _chk(x, name="x")
+        P = torch.empty((B, H, W, self.pcp), dtype=torch.float32, device=x.device)
+        nb = 4 * (x.numel() + P.numel())
+        profiling.timed_hbm("gdn+tap", nb, lambda: _lib.call(
+            "fvc_gdn_tap_nhwc", x.data_ptr(), P.data_ptr(), beta.data_ptr(), gamma.data_ptr(), self.wpack.data_ptr(),
+            ctypes.addressof(self.osc), self.ntiles, self.pcp, B, H, W, C, int(inverse),
+            overflow_flag(x.device).data_ptr(), stream_handle()))
+        ho, wo = (H * self.stride, W * self.stride) if self.transposed else (H, W)
+        y = torch.empty((B, ho, wo, cp4(self.cout)), dtype=torch.float32, device=x.device)
+        _chk(res, y.shape, name="res")
+        nb = 4 * (P.numel() + y.numel() * (2 if res is not None else 1))
+        profiling.timed_hbm("tap_gather", nb, lambda: _lib.call(
+            "fvc_tap_gather_nhwc", P.data_ptr(), self.pcp, self.bias.data_ptr(), _ptr(res), y.data_ptr(), B, H, W,
+            self.cout, self.ksize, self.stride, int(self.transposed), act, post, stream_handle()))
+        return y
+
+
 def x3_overflow(reset: bool = True, device=None) -> bool:
     """True if any split-precision conv on the current stream staged an activation with
     |v| >= 65000 since the last reset (waits for the stream's queued work)."""

@@ -64,6 +64,13 @@ class _ConvP(nn.Module):
                 self._packed["tap"] = None
         return self._packed["tap"]
 
+    def gdn_tap(self):
+        """This (cout <= 4, 64-input) layer fused behind a GDN kernel (cached)."""
+        if "gdntap" not in self._packed:
+            self._packed["gdntap"] = K.GdnTap(self.weight, self.bias, self.k, self.stride, self.transposed,
+                                              self.weight.device)
+        return self._packed["gdntap"]
+
     def invalidate(self):
         self._packed = {}
 
@@ -292,13 +299,15 @@ class Synthesis_net(nn.Module):
 
     def run(self, feature, prediction):
         x = feature
-        for i in range(1, 5):
-            x = getattr(self, f"deconv{i}").packed()(x, in_op=K.IN_ROUND if i == 1 else K.IN_NONE,
-                                                     res=prediction if i == 4 else None)
-            if i < 4:
-                b, g = getattr(self, f"igdn{i}").effective()
-                x = K.gdn(x, b, g, True)
-        return x
+        for i in range(1, 4):
+            x = getattr(self, f"deconv{i}").packed()(x, in_op=K.IN_ROUND if i == 1 else K.IN_NONE)
+            b, g = getattr(self, f"igdn{i}").effective()
+            if i == 3 and K.conv_precision() == "x3" and os.environ.get("FVC_GDN_TAP", "1") != "0":
+                # igdn3 feeds only deconv4 (64 -> 3): its 75 tap partials come out of the IGDN
+                # kernel and igdn3's output never reaches HBM (FVC_GDN_TAP=0: two launches)
+                return self.deconv4.gdn_tap()(x, b, g, True, res=prediction)
+            x = K.gdn(x, b, g, True)
+        return self.deconv4.packed()(x, res=prediction)
 
 
 class Analysis_prior_net(nn.Module):

@@ -176,6 +176,13 @@ int fvc_tap_gather_nhwc(const float* P, int pcp, const float* bias, const float*
  * beta/gamma are the effective (bounded, reparametrised) parameters: gamma[i*c + j] */
 int fvc_gdn_nhwc(const float* x, float* y, const float* beta, const float* gamma, int batch,
                  int h, int w, int c, int inverse, fvc_stream_t stream);
+/* GDN / IGDN of x (64 channels) followed by the next layer's 1x1 tap-partial GEMM: P [b][h][w][pcp]
+ * = tap_w . y with y never written (resDecoder igdn3 -> deconv4, synthesis.py:26,57); tap_wpack
+ * is ntiles concatenated fvc_x3_tap_pack_weight packs of 32 rows each (cin = 64), tap_osc
+ * (host, ntiles floats) their scales; |y| >= 65000 ORs 1 into *overflow_flag. */
+int fvc_gdn_tap_nhwc(const float* x, float* P, const float* beta, const float* gamma,
+                     const void* tap_wpack, const float* tap_osc, int ntiles, int pcp, int batch,
+                     int h, int w, int c, int inverse, int* overflow_flag, fvc_stream_t stream);
 
 /* ------------------------------------------------------------------ reductions
  * Deterministic (fixed-order, no atomics) two-pass reductions; ws must hold

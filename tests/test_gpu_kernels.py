@@ -202,6 +202,35 @@ def test_conv_then_tap_fused(dev, case, monkeypatch):
     close(from_nhwc(out2.cpu(), c2), from_nhwc(oc, c2), 2e-6)
 
 
+@pytest.mark.parametrize("inverse", [True, False])
+def test_gdn_then_tap_fused(dev, inverse, monkeypatch):
+    """IGDN / GDN (64 ch) with the next 64->3 5x5 s2 transposed conv's 75 tap partials computed
+    in the GDN kernel (fvc_gdn_tap_nhwc, 3 P tiles) + the transposed gather, against torch fp32
+    (GDN.py:63-93 then conv_transpose2d + residual), and the model path with and without the
+    fusion (FVC_GDN_TAP) on a decoder-sized call."""
+    g = torch.Generator().manual_seed(21 + int(inverse))
+    B, H, W = 2, 13, 22
+    x = torch.randn(B, 64, H, W, generator=g)
+    beta = torch.rand(64, generator=g) + 0.5
+    gamma = torch.rand(64, 64, generator=g) * 0.05 + torch.eye(64) * 0.2
+    w = torch.randn(64, 3, 5, 5, generator=g) * (1.0 / (64 * 25) ** 0.5)
+    b = torch.randn(3, generator=g) * 0.1
+    norm = torch.sqrt(F.conv2d(x * x, gamma[:, :, None, None], beta))
+    y = x * norm if inverse else x / norm
+    ref = F.conv_transpose2d(y, w, b, 2, 2, 1)
+    res = torch.randn(ref.shape, generator=g)
+    ref = ref + res
+    t = K.GdnTap(w, b, 5, 2, True, dev)
+    assert (t.np, t.pcp, t.ntiles) == (75, 76, 3)
+    K.x3_overflow(reset=True)
+    out = t(to_nhwc(x).to(dev), beta.to(dev), gamma.to(dev).contiguous(), inverse, res=to_nhwc(res).to(dev))
+    torch.cuda.synchronize()
+    assert not K.x3_overflow(reset=True)
+    oc = out.cpu()
+    close(from_nhwc(oc, 3), ref, 2e-5)
+    assert float(oc[..., 3:].abs().max()) == 0.0
+
+
 @pytest.mark.parametrize("shape", [(2, 64, 64, 38, 70), (1, 64, 64, 33, 45), (3, 32, 64, 16, 32), (2, 64, 32, 20, 96)])
 @pytest.mark.parametrize("with_res", [False, True])
 def test_conv_x3_pool_epilogue(dev, shape, with_res, monkeypatch):
