@@ -159,12 +159,13 @@ __global__ __launch_bounds__(256) void k_tap_gather3_lds(const float* __restrict
 // Transposed (stride 2, output padding 1) tap gather through LDS: a block's 16 x 32 outputs read
 // input rows Y0/2 - 1 .. Y0/2 + 8 and columns X0/2 - 1 .. X0/2 + 17 of P (k = 3 or 5), staged
 // once with coalesced 16-B loads; per output the same tap order as k_tap_gather.
-template <int KS, int COUT>
+template <int KS, int COUT, int TH>
 __global__ __launch_bounds__(256) void k_tap_gather_t2_lds(const float* __restrict__ P, int pcp,
                                                            const float* __restrict__ bias,
                                                            const float* __restrict__ res, float* __restrict__ y,
                                                            int H, int W, float act_slope, int post_op) {
-  constexpr int TH = 16, TW = 32, IR = 10, IC = 19, pad = KS / 2;
+  // output rows Y0 .. Y0 + TH - 1 read input rows Y0/2 - 1 .. Y0/2 + TH/2 (k <= 5)
+  constexpr int TW = 32, IR = TH / 2 + 2, IC = 19, pad = KS / 2;
   extern __shared__ float sp[];
   const int ps = pcp + 1;
   const int c4n = pcp >> 2;
@@ -998,15 +999,22 @@ int fvc_tap_gather_nhwc(const float* P, int pcp, const float* bias, const float*
 #undef FVC_TGL
   }
   if (transposed && pcp <= 128) {
-    const dim3 gt(fvc_cdiv(Wo, 32), fvc_cdiv(Ho, 16), batch);
-    const size_t lds = (size_t)10 * 19 * (pcp + 1) * 4;
+    // 8-row output tiles (6 x 19 input pixels in LDS: ~35 KB at pcp 76, four blocks per CU);
+    // FVC_GATHER_TH=16: 16-row tiles
+    const char* th_env = getenv("FVC_GATHER_TH");
+    const int th = (th_env && atoi(th_env) == 16) ? 16 : 8;
+    const dim3 gt(fvc_cdiv(Wo, 32), fvc_cdiv(Ho, th), batch);
+    const size_t lds = (size_t)(th / 2 + 2) * 19 * (pcp + 1) * 4;
 #define FVC_TGT(KS, CO)                                                                                        \
     if (ksize == KS && cout == CO) {                                                                          \
-      if (lds > 64 * 1024)                                                                                    \
-        (void)hipFuncSetAttribute((const void*)k_tap_gather_t2_lds<KS, CO>,                                   \
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                      \
-      hipLaunchKernelGGL((k_tap_gather_t2_lds<KS, CO>), gt, dim3(256), lds, st, P, pcp, bias, res, y, h, w, slope, \
-                         post_op);                                                                            \
+      const void* fn = th == 8 ? (const void*)k_tap_gather_t2_lds<KS, CO, 8> : (const void*)k_tap_gather_t2_lds<KS, CO, 16>; \
+      if (lds > 64 * 1024) (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); \
+      if (th == 8)                                                                                            \
+        hipLaunchKernelGGL((k_tap_gather_t2_lds<KS, CO, 8>), gt, dim3(256), lds, st, P, pcp, bias, res, y, h, w, \
+                           slope, post_op);                                                                   \
+      else                                                                                                    \
+        hipLaunchKernelGGL((k_tap_gather_t2_lds<KS, CO, 16>), gt, dim3(256), lds, st, P, pcp, bias, res, y, h, w, \
+                           slope, post_op);                                                                   \
       FVC_CHECK_LAUNCH();                                                                                     \
       return 0;                                                                                               \
     }
