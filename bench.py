@@ -29,7 +29,9 @@ import argparse
 import json
 import math
 import os
+import socket
 import statistics
+import subprocess
 import sys
 import time
 
@@ -50,6 +52,7 @@ ENC_TFLOP_1088 = 2.931
 DEC_TFLOP_1088 = 1.295
 AREA_1088 = 1920 * 1088
 METRIC_1080 = "1080p frames/sec encode+decode at λ=1024; bpp/PSNR parity vs CPU ref"
+ONE_THREAD_1080_BUDGET_S = 240.0  # cap on the CPU leg's 1-thread 1080p run
 
 
 def tflop_per_pframe(hp, wp):
@@ -91,9 +94,10 @@ def cpu_baseline(model, dev, frames_np, mode="quick"):
     golden fixtures) + the C oracle coder on the host cores, and the parity block of the same
     frame (GOP 0, frame 1 coded against frame 0, which the GPU run also codes first).
 
-    quick (default, ~30 s of CPU work): 1080p encode+decode once at all cores (the parity sample),
-    256x256 forward median of 3 after a warm-up at all cores and at 1 thread, C coder on one core.
-    full: additionally a warm-up and a median of 3 at 1080p, and 1080p at 1 thread."""
+    full (default; ~3 min of CPU work): 256x256 forward median of 3 after a warm-up at
+    all cores and at 1 thread; 1080p encode+decode median of 3 after a warm-up at all cores, and once
+    at 1 thread (skipped, and said so, if predicted over ONE_THREAD_1080_BUDGET_S); C coder on one core.
+    quick (~30 s): 1080p once at all cores (the parity sample) instead of the 1080p protocol."""
     from oracle import coder_ref as R
     from oracle import dvc_ref
     from fastvideocodec_amd.synthetic import make_gop
@@ -112,16 +116,6 @@ def cpu_baseline(model, dev, frames_np, mode="quick"):
         dvc_ref.decode(sd, ref, inter["quant_mv"], inter["compressed_z"], inter["compressed_feature"])
         state["out"], state["inter"] = out, inter
 
-    full = mode == "full"
-    if full:
-        enc_dec()  # warm-up
-    t_1080, runs_1080 = _median_time(enc_dec, 3 if full else 1)
-    one_thread_1080 = None
-    if full:
-        torch.set_num_threads(1)
-        one_thread_1080 = _median_time(enc_dec, 1)[0]
-        torch.set_num_threads(cores)
-
     small = make_gop(256, 256, 2, 20261015)
     c1, r1 = torch.from_numpy(small[1:2].copy()), torch.from_numpy(small[0:1].copy())
     f256 = lambda: dvc_ref.forward(sd, c1, r1)
@@ -131,6 +125,23 @@ def cpu_baseline(model, dev, frames_np, mode="quick"):
     f256()
     t_256_1 = _median_time(f256, 3)[0]
     torch.set_num_threads(cores)
+
+    full = mode == "full"
+    if full:
+        enc_dec()  # warm-up
+    t_1080, runs_1080 = _median_time(enc_dec, 3 if full else 1)
+    one_thread_1080 = None
+    one_thread_note = None
+    if full:
+        # the 1-thread 1080p run is bounded so the default bench stays within a few minutes: its
+        # length is predicted from the all-core 1080p median and the 256x256 thread-scaling ratio
+        est = t_1080 * t_256_1 / max(t_256, 1e-9)
+        if est <= ONE_THREAD_1080_BUDGET_S:
+            torch.set_num_threads(1)
+            one_thread_1080 = _median_time(enc_dec, 1)[0]
+            torch.set_num_threads(cores)
+        else:
+            one_thread_note = f"skipped: predicted {est:.0f} s > {ONE_THREAD_1080_BUDGET_S:.0f} s budget"
 
     parity, coder = parity_block(model, dev, cur, ref, state["out"], state["inter"], R)
     cpu_model = ""
@@ -149,6 +160,8 @@ def cpu_baseline(model, dev, frames_np, mode="quick"):
            "coder_1core": coder}
     if one_thread_1080 is not None:
         res["seconds_1080_1thread"] = round(one_thread_1080, 2)
+    if one_thread_note:
+        res["seconds_1080_1thread"] = one_thread_note
     return res, parity
 
 
@@ -238,6 +251,7 @@ class GpuGopJob:
         else:
             mine = fdist.shard_gops(world * args.gops_per_gpu, rank, world)  # GOP g -> rank g % world
             gops = [make_gop(args.height, args.width, args.gop, gop_seed(g)) for g in mine]
+        self.shard = mine  # GOP (or view) ids this rank codes
         self.gops_np = gops
         self.units = len(gops)
         self.frames = torch.from_numpy(np.stack(gops)).to(dev)  # [G, T, 3, Hp, Wp]
@@ -246,7 +260,10 @@ class GpuGopJob:
     def step(self):
         if self.args.tree:
             from fastvideocodec_amd.tree_gop import encode_decode_tree_gop
-            encode_decode_tree_gop(self.model, self.frames, overlap=not self.args.serial)
+            # streamed like the linear GOP: no per-step host wait, overflow probes resolved in
+            # after_timing (gop.check_overflow); past 31 P-frames the 62-frame binary tree
+            encode_decode_tree_gop(self.model, self.frames, overlap=not self.args.serial, join=False,
+                                   extend=True)
             return
         from fastvideocodec_amd.gop import encode_decode_gop
         encode_decode_gop(self.model, self.frames, overlap=not self.args.serial, join=False)
@@ -256,7 +273,7 @@ class GpuGopJob:
 
     def _tree_layers(self):
         from fastvideocodec_amd.tree_gop import coding_layers
-        return coding_layers(self.args.gop - 1)
+        return coding_layers(self.args.gop - 1, extend=True)
 
     def after_timing(self):
         """Roofline pass: one serial GOP (single stream) with HIP events around every launch on
@@ -281,7 +298,7 @@ class GpuGopJob:
         if self.args.tree:
             from fastvideocodec_amd.tree_gop import encode_decode_tree_gop
             bss, dd, sses, ee = encode_decode_tree_gop(self.model, self.frames, check=True,
-                                                       overlap=not self.args.serial)
+                                                       overlap=not self.args.serial, extend=True)
             decoded, encs = [dd[t] for t in sorted(dd)], [ee[t] for t in sorted(ee)]
             sses = [s / len(lay) for s, lay in zip(sses, self._tree_layers())]  # per-frame mean SSE
         else:
@@ -295,6 +312,38 @@ class GpuGopJob:
         return {"bitexact": all(torch.equal(a, b) for a, b in zip(decoded, encs)),
                 "nbytes": sum(b.nbytes() for b in bss), "psnr": float(np.mean(psnrs)), "payload": payload,
                 "overflow_recomputes": getattr(self.model, "overflow_events", 0) - overflow_before}
+
+
+class HostRehearsalJob:
+    """`--dry-run`: the per-rank job's interface with host-only work (no GPU, no codec), so the
+    launcher, the rank partitioning and the collectives can be rehearsed under gloo on CPU
+    (tests/test_bench_dist.py). Its numbers measure nothing."""
+
+    def __init__(self, args, rank, world):
+        self.args = args
+        if args.views > 0:
+            if args.views < world:
+                raise SystemExit(f"--views {args.views} < world size {world}: a rank would have no view")
+            self.shard = fdist.shard_views(args.views, rank, world)
+        else:
+            self.shard = fdist.shard_gops(world * args.gops_per_gpu, rank, world)
+        self.units = len(self.shard)
+        self.Hp, self.Wp = (args.height + 63) // 64 * 64, (args.width + 63) // 64 * 64
+        self.rank = rank
+
+    def step(self):
+        time.sleep(0.005 * (1 + self.rank))
+
+    def sync(self):
+        pass
+
+    def after_timing(self):
+        return None
+
+    def verify(self):
+        payload = b"".join(bytes([u % 256]) * (100 + u) for u in self.shard)
+        return {"bitexact": True, "nbytes": len(payload), "psnr": 30.0, "payload": payload,
+                "overflow_recomputes": 0}
 
 
 def run_rank(job, args, rank, world, device):
@@ -319,8 +368,9 @@ def run_rank(job, args, rank, world, device):
     ver = job.verify()
     dt_max = fdist.max_over_ranks(dt, device)
     allst = fdist.gather_stats([1.0 if ver["bitexact"] else 0.0, float(ver["nbytes"]), ver["psnr"],
-                                float(job.units)], device)
+                                float(job.units), float(ver["overflow_recomputes"])], device)
     gathered = fdist.gather_bytes(ver["payload"], device, dst=0)
+    shards = fdist.gather_bytes(json.dumps(list(getattr(job, "shard", []))).encode(), device, dst=0)
     if rank != 0:
         return None
     units = int(allst[:, 3].sum())
@@ -353,13 +403,15 @@ def run_rank(job, args, rank, world, device):
                     "views": args.views, "views_per_gpu": job.units,
                     "frames_counted": "P-frames only (I-frame pass-through)",
                     "parallelism": f"view-shard x{world}"}),
+        "shards": {"unit": "view" if args.views > 0 else "gop",
+                   "by_rank": [json.loads(s.decode()) for s in shards]},
         "model_tflop_per_pframe": round(enc_tf + dec_tf, 3),
         "effective_tflops": round(value / world * (enc_tf + dec_tf), 2),
         "quality": {"decoder_bitexact": bitexact_all,
                     "bytes_per_pframe": round(bytes_all / pframes_per_step, 1),
                     "bpp_actual": round(bytes_all * 8 / (pframes_per_step * job.Hp * job.Wp), 5),
                     "psnr_db_mean": round(float(np.mean(allst[:, 2])), 4),
-                    "overflow_recomputes": ver["overflow_recomputes"],
+                    "overflow_recomputes": int(allst[:, 4].sum()),
                     "bitstreams_gathered_to_rank0_bytes": sum(len(g) for g in gathered),
                     "note": "seeded (untrained) codec weights + synthetic GOP: PSNR/bpp are not rate-distortion "
                             "figures; the coder's symbol statistics (and so its timing) are those of untrained "
@@ -440,9 +492,9 @@ def parse_args(argv=None):
     ap.add_argument("--views", type=int, default=0,
                     help="BASELINE configs[4]: V camera views, one GOP stream each, view v -> rank v %% world "
                          "(replaces --gops-per-gpu; the reference's MCVC couples views, DVC views are independent)")
-    ap.add_argument("--cpu-baseline", choices=("quick", "full", "none"), default="quick",
-                    help="CPU leg + parity block on rank 0 at N=1: quick (~30 s), full (BASELINE.md §3 protocol, "
-                         "several minutes), none")
+    ap.add_argument("--cpu-baseline", choices=("quick", "full", "none"), default="full",
+                    help="CPU leg + parity block on rank 0 at N=1: full (default; BASELINE.md §3 protocol, "
+                         "~3 min), quick (~30 s), none")
     ap.add_argument("--no-cpu-baseline", action="store_true", help="same as --cpu-baseline none")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--breakdown", action="store_true", help="print per-conv-geometry timing to stderr")
@@ -452,24 +504,78 @@ def parse_args(argv=None):
                          "sequential DVC GOP; reported separately)")
     ap.add_argument("--serial", action="store_true",
                     help="one HIP stream (no encode/code/decode overlap): per-kernel durations are unshared")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="rehearse the launcher, sharding and collectives on CPU (gloo) with a host job: "
+                         "no GPU work, the numbers measure nothing")
     args = ap.parse_args(argv)
     if args.no_cpu_baseline:
         args.cpu_baseline = "none"
     return args
 
 
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(n, argv):
+    """`python bench.py --gpus N` outside a launcher: start N fresh rank processes (this parent
+    never touches the GPU, so no process that has initialised HIP is replaced), one per GPU,
+    with the torchrun environment (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*, rendezvous on
+    127.0.0.1). Only rank 0 prints. If a rank fails, the others are stopped (their exact PIDs).
+    Returns the first non-zero exit status, or 0."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in live:
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
+
+
 def main(argv=None):
+    argv = list(sys.argv[1:] if argv is None else argv)
     args = parse_args(argv)
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return spawn_ranks(args.gpus, argv)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
-    job = GpuGopJob(args, rank, world, dev)
+    if world != args.gpus:
+        # a result must never mislabel its rank count
+        raise SystemExit(f"--gpus {args.gpus} != WORLD_SIZE {world} set by the launcher")
+    if args.dry_run:
+        if world > 1:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+        job, dev = HostRehearsalJob(args, rank, world), None
+    else:
+        if world > 1:
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dev = torch.device("cuda", local)
+        job = GpuGopJob(args, rank, world, dev)
     result = run_rank(job, args, rank, world, dev)
-    if rank == 0 and world == 1 and args.cpu_baseline != "none":
+    if args.dry_run and rank == 0:
+        result["data"] = "dry run: host rehearsal job, no GPU work (launcher / sharding / collectives only)"
+    if rank == 0 and world == 1 and args.cpu_baseline != "none" and not args.dry_run:
         cb, parity = cpu_baseline(job.model, dev, job.gops_np[0], args.cpu_baseline)
         result["cpu_baseline"] = cb
         result["quality"]["parity"] = parity
@@ -481,7 +587,8 @@ def main(argv=None):
                 f.write(line + "\n")
     if world > 1:
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -349,6 +349,7 @@ constexpr int kTabDir = 256;          // cached tables at most
 constexpr int kTabWords = 25600;      // 100 KB of table images
 constexpr size_t kDec2Lds =
     (size_t)(2 * kJ * 64 * 4 + 2 * kJ * 64 + kR * 64 + 3 * 64 + 4 + 2 * kTabDir + kTabWords) * 4;
+static_assert(kDec2Lds <= 160 * 1024, "k_rans_decode's LDS image must fit gfx950's 160 KB per CU");
 constexpr uint32_t kGlobTab = 0x80000000u;  // record flag: table image read from global memory
 constexpr int kDecSpb = 64;                 // streams per decode block when the caller passes 0
 constexpr int kRsrcFlags = 0x00020000;  // buffer descriptor dword 3 (raw 32-bit, as fvc_conv_x3.hip)
@@ -732,8 +733,12 @@ int fvc_rans_decode(const uint32_t* packed, const int64_t* pack_off, const int32
       nstreams <= 0 || ntables <= 0 || cdf_stride <= 1)
     return FVC_EINVAL;
   const uint32_t* img_off = (const uint32_t*)lut;
-  (void)hipFuncSetAttribute((const void*)k_rans_decode, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kDec2Lds);
   if (streams_per_block < 0 || streams_per_block > 64) return FVC_EINVAL;
+  // kDec2Lds (static_assert'ed against gfx950's 160 KB per CU above) needs the opt-in: a device
+  // that refuses it cannot run this kernel, so report that instead of a generic launch failure
+  const hipError_t attr =
+      hipFuncSetAttribute((const void*)k_rans_decode, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kDec2Lds);
+  if (attr != hipSuccess) return -(int)attr;
   const int spb = streams_per_block ? streams_per_block : kDecSpb;
   hipLaunchKernelGGL(k_rans_decode, dim3((nstreams + spb - 1) / spb), dim3(128), kDec2Lds, (hipStream_t)s, packed,
                      pack_off, indexes, sym_off, nstreams, cdf_sizes, offsets, ntables, img_off, img_off + ntables + 1,

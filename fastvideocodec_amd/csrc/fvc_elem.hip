@@ -664,7 +664,7 @@ __global__ __launch_bounds__(kBlk) void k_recon_finalize(const float* __restrict
                                                          const float* __restrict__ wf, const float* __restrict__ pred,
                                                          float* __restrict__ clipped, double* __restrict__ ws,
                                                          int B, int H, int W) {
-  double acc[3] = {0.0, 0.0, 0.0};
+  double acc[4] = {0.0, 0.0, 0.0, 0.0};
   const size_t npix = (size_t)B * H * W;
   const size_t hw = (size_t)H * W;
   for (size_t p = grid_stride_start(); p < npix; p += (size_t)gridDim.x * blockDim.x) {
@@ -681,10 +681,13 @@ __global__ __launch_bounds__(kBlk) void k_recon_finalize(const float* __restrict
       acc[0] += (double)(d0 * d0);
       acc[1] += (double)(d1 * d1);
       acc[2] += (double)(d2 * d2);
-      clipped[(b * 3 + c) * hw + q] = fminf(fmaxf(rr[c], 0.f), 1.f);
+      const float cv = fminf(fmaxf(rr[c], 0.f), 1.f);
+      const float d3 = cv - xx[c];
+      acc[3] += (double)(d3 * d3);
+      clipped[(b * 3 + c) * hw + q] = cv;
     }
   }
-  block_reduce_store<3>(acc, ws);
+  block_reduce_store<4>(acc, ws);
 }
 
 // Laplace bits (net.py:121-151): p = cdf(f+.5) - cdf(f-.5), cdf(v) = .5 - .5 sign(v) expm1(-|v|/s)
@@ -1141,12 +1144,12 @@ int fvc_gdn_tap_nhwc(const float* x, float* P, const float* beta, const float* g
 size_t fvc_reduce_ws_doubles(void) { return (size_t)kRedBlocks * 4; }
 
 int fvc_recon_finalize(const float* recon, const float* input, const float* warpframe, const float* prediction,
-                       float* clipped, double* out3, double* ws, int batch, int h, int w, fvc_stream_t s) {
-  if (!recon || !input || !warpframe || !prediction || !clipped || !out3 || !ws) return FVC_EINVAL;
+                       float* clipped, double* out4, double* ws, int batch, int h, int w, fvc_stream_t s) {
+  if (!recon || !input || !warpframe || !prediction || !clipped || !out4 || !ws) return FVC_EINVAL;
   hipLaunchKernelGGL(k_recon_finalize, dim3(kRedBlocks), dim3(kBlk), 0, (hipStream_t)s, recon, input, warpframe,
                      prediction, clipped, ws, batch, h, w);
   FVC_CHECK_LAUNCH();
-  hipLaunchKernelGGL(k_reduce_partials<3>, dim3(1), dim3(kBlk), 0, (hipStream_t)s, ws, kRedBlocks, out3);
+  hipLaunchKernelGGL(k_reduce_partials<4>, dim3(1), dim3(kBlk), 0, (hipStream_t)s, ws, kRedBlocks, out4);
   FVC_CHECK_LAUNCH();
   return 0;
 }

@@ -548,13 +548,13 @@ def recon_finalize(recon, inp, warpframe, prediction):
     for t, n in ((recon, "recon"), (inp, "input"), (warpframe, "warpframe"), (prediction, "prediction")):
         _chk(t, (B, H, W, 4), name=n)
     clipped = torch.empty((B, 3, H, W), dtype=torch.float32, device=recon.device)
-    out3 = torch.empty(3, dtype=torch.float64, device=recon.device)
+    out4 = torch.empty(4, dtype=torch.float64, device=recon.device)  # recon, warp, pred, clipped SSEs
     nb = 4 * (recon.numel() + inp.numel() + warpframe.numel() + prediction.numel() + clipped.numel())
     ws = _ws(recon.device)
     profiling.timed_hbm("recon_finalize", nb, lambda: _lib.call(
         "fvc_recon_finalize", recon.data_ptr(), inp.data_ptr(), warpframe.data_ptr(), prediction.data_ptr(),
-        clipped.data_ptr(), out3.data_ptr(), ws.data_ptr(), B, H, W, stream_handle()))
-    return clipped, out3
+        clipped.data_ptr(), out4.data_ptr(), ws.data_ptr(), B, H, W, stream_handle()))
+    return clipped, out4
 
 
 def bits_laplace(feature, sigma, c):

@@ -36,20 +36,26 @@ from .weights import OUT_CHANNEL_M, OUT_CHANNEL_MV, OUT_CHANNEL_N
 class _ConvP(nn.Module):
     """Parameters of an nn.Conv2d / nn.ConvTranspose2d (same names/shapes as torch)."""
 
-    def __init__(self, cin, cout, k, stride=1, transposed=False):
+    def __init__(self, cin, cout, k, stride=1, transposed=False, bias=True):
         super().__init__()
         shape = (cin, cout, k, k) if transposed else (cout, cin, k, k)
         self.weight = Parameter(torch.zeros(shape), requires_grad=False)
-        self.bias = Parameter(torch.zeros(cout), requires_grad=False)
+        # bias=False: no `bias` entry in the state_dict (nn.Conv2d(..., bias=False)); the kernels
+        # get a zero bias vector
+        self.bias = Parameter(torch.zeros(cout), requires_grad=False) if bias else None
+        self.cout = cout
         self.k, self.stride, self.transposed = k, stride, transposed
         self._packed = {}
+
+    def _bias(self):
+        return self.bias if self.bias is not None else torch.zeros(self.cout, device=self.weight.device)
 
     def packed(self) -> K.PackedConv:
         """The weight pack for the active conv precision (x3 by default; f32 when a frame is
         recomputed after a split-precision overflow), built once per precision."""
         p = K.conv_precision()
         if p not in self._packed:
-            self._packed[p] = K.PackedConv(self.weight, self.bias, self.k, self.stride, self.transposed,
+            self._packed[p] = K.PackedConv(self.weight, self._bias(), self.k, self.stride, self.transposed,
                                            self.weight.device, precision=p)
         return self._packed[p]
 
@@ -58,7 +64,7 @@ class _ConvP(nn.Module):
         None when it has more than 32 partials (k*k*cout)."""
         if "tap" not in self._packed:
             try:
-                self._packed["tap"] = K.TapConsumer(self.weight, self.bias, self.k, self.stride, self.transposed,
+                self._packed["tap"] = K.TapConsumer(self.weight, self._bias(), self.k, self.stride, self.transposed,
                                                     self.weight.device)
             except ValueError:
                 self._packed["tap"] = None
@@ -67,7 +73,7 @@ class _ConvP(nn.Module):
     def gdn_tap(self):
         """This (cout <= 4, 64-input) layer fused behind a GDN kernel (cached)."""
         if "gdntap" not in self._packed:
-            self._packed["gdntap"] = K.GdnTap(self.weight, self.bias, self.k, self.stride, self.transposed,
+            self._packed["gdntap"] = K.GdnTap(self.weight, self._bias(), self.k, self.stride, self.transposed,
                                               self.weight.device)
         return self._packed["gdntap"]
 

@@ -21,6 +21,7 @@ fixtures, tests/golden/rlvc_rpm.npz).
 from __future__ import annotations
 
 import math
+import os
 
 import numpy as np
 import torch
@@ -29,6 +30,7 @@ from torch.nn import Parameter
 
 from . import _lib
 from . import kernels as K
+from ._lib import FvcError
 from .entropy_models import ConditionalEntropyModel, _CompressaiEntropyModel, _pack_tables, get_scale_table
 from .net import ME_Spynet, Warp_net, _ConvP, _GDNP
 
@@ -53,16 +55,18 @@ class ConvLSTM(nn.Module):
         self.conv = _ConvP(2 * channels, 4 * channels, 3)
         self._forget_bias = float(forget_bias)
         self._channels = channels
-        self._packs = None
+        self._packs = {}
 
     def invalidate(self):
-        self._packs = None
+        self._packs = {}
 
     def _gate_convs(self):
-        if self._packs is None:
+        """Per gate (x-part, h-part) packs for the active conv precision (cached per precision, so
+        a frame recomputed under ``K.precision('f32')`` runs its gates on the fp32 kernels too)."""
+        p = K.conv_precision()
+        if p not in self._packs:
             C = self._channels
             w, b = self.conv.weight, self.conv.bias
-            p = K.conv_precision()
             packs = []
             for g in range(4):
                 wg = w[g * C:(g + 1) * C]
@@ -70,8 +74,8 @@ class ConvLSTM(nn.Module):
                                            precision=p),
                               K.PackedConv(wg[:, C:].contiguous(), torch.zeros(C, device=w.device), 3, 1, False,
                                            w.device, precision=p)))
-            self._packs = packs
-        return self._packs
+            self._packs[p] = packs
+        return self._packs[p]
 
     def run(self, x, state):
         """x [B,H,W,C]; state {'c', 'h'} -> (h, new state)."""
@@ -94,18 +98,18 @@ class RPM(nn.Module):
         self.conv8 = _ConvP(channels, 2 * channels, 3)
         self.channels = channels
         self.lstm = ConvLSTM(channels)
-        self._split = None
+        self._split = {}
 
     def invalidate(self):
-        self._split = None
+        self._split = {}
 
     def _conv8(self):
-        if self._split is None:
+        p = K.conv_precision()
+        if p not in self._split:
             C, w, b = self.channels, self.conv8.weight, self.conv8.bias
-            p = K.conv_precision()
-            self._split = tuple(K.PackedConv(w[i * C:(i + 1) * C].contiguous(), b[i * C:(i + 1) * C], 3, 1, False,
-                                             w.device, precision=p) for i in range(2))
-        return self._split
+            self._split[p] = tuple(K.PackedConv(w[i * C:(i + 1) * C].contiguous(), b[i * C:(i + 1) * C], 3, 1,
+                                                False, w.device, precision=p) for i in range(2))
+        return self._split[p]
 
     def run(self, prior, hidden, round_input=True):
         """prior: the previous frame's latent (rounded here, as entropy_models.py:67 / :122 do
@@ -145,6 +149,7 @@ class LearnedEntropyBottleneck(_CompressaiEntropyModel, nn.Module):
     def invalidate(self):
         self._prm = None
         self._coder = None
+        self._aux = None
 
     def kernel_params(self):
         """[C, 58] softplus(matrices), biases, tanh(factors) + medians [C] (device)."""
@@ -159,6 +164,17 @@ class LearnedEntropyBottleneck(_CompressaiEntropyModel, nn.Module):
             dev = self.quantiles.device
             self._prm = (prm.to(dev), self.quantiles[:, 0, 1].detach().float().contiguous().to(dev))
         return self._prm
+
+    def loss(self):
+        """compressai ``EntropyBottleneck.loss()``: sum |logits_cumulative(quantiles) - target|,
+        target = (-t, 0, t), t = log(2 / tail_mass - 1) (tail_mass 1e-9). A function of the
+        parameters only (host, float32, like ``update()``); cached until the weights change."""
+        if getattr(self, "_aux", None) is None:
+            t = float(np.log(2 / 1e-9 - 1))
+            target = torch.tensor([-t, 0.0, t], dtype=torch.float32)
+            logits = self._logits_cumulative(self.quantiles.detach().cpu().float())
+            self._aux = torch.abs(logits - target).sum().to(self.quantiles.device)
+        return self._aux
 
     def _logits_cumulative(self, inputs):
         logits = inputs
@@ -275,6 +291,12 @@ class RecProbModel(nn.Module):
     def get_actual_bits(strings):
         return float(len(b"".join(strings)) * 8)
 
+    def loss(self):
+        """entropy_models.py:50-53: 0 in RPM mode, else the bottleneck's auxiliary loss."""
+        if self.RPM_flag:
+            return torch.zeros((), device=self.entropy_bottleneck.quantiles.device)
+        return self.entropy_bottleneck.loss()
+
 
 class Coder2D(nn.Module):
     """models.py:520-681 with keyword 'RLVC' (downsample, conv_type 'rec', entropy 'rpm')."""
@@ -284,7 +306,9 @@ class Coder2D(nn.Module):
         if keyword not in ("RLVC", "rpm"):
             raise ValueError(f"Coder2D keyword {keyword!r}: only the RLVC recurrent model is built")
         for i in range(1, 5):
-            setattr(self, f"enc_conv{i}", _ConvP(in_channels if i == 1 else channels, channels, kernel, 2))
+            # enc_conv4 has no bias in the reference (models.py:528)
+            setattr(self, f"enc_conv{i}", _ConvP(in_channels if i == 1 else channels, channels, kernel, 2,
+                                                 bias=i != 4))
             setattr(self, f"dec_conv{i}", _ConvP(channels, in_channels if i == 4 else channels, kernel, 2,
                                                  transposed=True))
         for i in range(1, 4):
@@ -321,6 +345,7 @@ class Coder2D(nn.Module):
         strings = eb.compress(latent) if real else None
         bits_act = eb.get_actual_bits(strings) if real else float(bits_est.item())
         hat, dec = self.decode(latent_hat, rae_hidden["dec"], res=res)
+        self.aux_loss = eb.loss()  # models.py:679
         return hat, {"enc": enc, "dec": dec}, rpm_hidden, bits_act, bits_est, prior_latent, strings
 
 
@@ -365,15 +390,39 @@ class RLVC(nn.Module):
         rae = lambda: {"enc": {"c": z(4), "h": z(4)}, "dec": {"c": z(4), "h": z(4)}}
         return rae(), rae(), {"c": z(16), "h": z(16)}, {"c": z(16), "h": z(16)}
 
+    # split-precision overflow: as VideoCompressor._run_checked -- every x3 conv ORs into the
+    # stream's flag; a frame that set it is recomputed on the fp32 kernels (or rejected)
+    on_overflow = "recompute"
+
     def forward(self, Y0_com, Y1_raw, hidden_states, RPM_flag, mv_prior_latent, res_prior_latent, real=True):
         """models.py:982-1040 (eval): -> (Y1_com, hidden_states, bpp_est, img_loss, aux_loss,
         bpp_act, psnr, mv_prior_latent, res_prior_latent); frames NCHW [B,3,H,W], H, W multiples of
-        64. ``self.last_strings`` holds the frame's (mv, res) strings."""
+        64. ``self.last_strings`` holds the frame's (mv, res) strings; ``self.last_precision`` the
+        conv precision the frame was coded with ('x3', or 'f32' after an overflow recompute).
+        ConvLSTM's cell state carries across frames unbounded, so the overflow check matters here."""
         if self.mv_codec.entropy_bottleneck.entropy_bottleneck._coder is None:
             self.update(force=True)
         B, _, H, W = Y1_raw.shape
         if H % 64 or W % 64:
             raise ValueError("H and W must be multiples of 64")
+        args = (Y0_com, Y1_raw, hidden_states, RPM_flag, mv_prior_latent, res_prior_latent, real)
+        if K.conv_precision() == "f32":
+            self.last_precision = "f32"
+            return self._forward_impl(*args)
+        K.overflow_flag().zero_()
+        out = self._forward_impl(*args)
+        if not K.OverflowProbe().result():
+            self.last_precision = "x3"
+            return out
+        self.overflow_events = getattr(self, "overflow_events", 0) + 1
+        if self.on_overflow == "raise":
+            raise FvcError("split-precision conv operand overflow (|activation| >= 65000) in RLVC")
+        with K.precision("f32"):
+            self.last_precision = "f32"
+            return self._forward_impl(*args)
+
+    def _forward_impl(self, Y0_com, Y1_raw, hidden_states, RPM_flag, mv_prior_latent, res_prior_latent, real):
+        B, _, H, W = Y1_raw.shape
         rae_mv, rae_res, rpm_mv, rpm_res = hidden_states
         with torch.no_grad():
             cur4 = K.nchw_to_nhwc(Y1_raw.float().contiguous(), 4)
@@ -388,12 +437,14 @@ class RLVC(nn.Module):
                 res, rae_res, rpm_res, RPM_flag, res_prior_latent, res=Y1_MC, real=real)
             clipped, sse = K.recon_finalize(recon, cur4, warpframe, Y1_MC)
         npx = B * H * W
-        img_loss = (sse[0] / (3 * npx)).float()
+        # img_loss / PSNR of the clipped Y1_com (models.py:1019,1033-1034): recon_finalize's 4th SSE
+        img_loss = (sse[3] / (3 * npx)).float()
         psnr = 10.0 * torch.log10(1.0 / img_loss)
         bpp_est = ((mv_est + res_est) / npx).float()[0]
         bpp_act = torch.tensor((mv_act + res_act) / npx)
         self.last_strings = (mv_str, res_str)
-        aux_loss = torch.zeros((), device=Y1_raw.device)
+        # models.py:1030-1031 at stage 'REC' (init_training_params, models.py:70): mv_aux + res_aux / 2
+        aux_loss = self.mv_codec.aux_loss + self.res_codec.aux_loss / 2
         return (clipped, (rae_mv, rae_res, rpm_mv, rpm_res), bpp_est, img_loss, aux_loss, bpp_act, psnr,
                 mv_prior_latent, res_prior_latent)
 
@@ -435,8 +486,8 @@ def seeded_state_dict(seed: int = 20261016, dvc_seed: int = 20261015):
             ci = cin if i == 1 else C
             # the last encoder conv is scaled so that latents span a few quantisation steps
             sd[f"{name}.enc_conv{i}.weight"] = _xavier_normal(rng, (C, ci, k, k), math.sqrt(2.0) * (12.0 if i == 4 else 1.0))
-            sd[f"{name}.enc_conv{i}.bias"] = (np.zeros(C, np.float32) if i == 4
-                                              else rng.uniform(-0.05, 0.05, C).astype(np.float32))
+            if i != 4:  # enc_conv4 is bias-free (models.py:528)
+                sd[f"{name}.enc_conv{i}.bias"] = rng.uniform(-0.05, 0.05, C).astype(np.float32)
             co = cin if i == 4 else C
             sd[f"{name}.dec_conv{i}.weight"] = _xavier_normal(rng, (C, co, k, k), 1.0)
             sd[f"{name}.dec_conv{i}.bias"] = rng.uniform(-0.05, 0.05, co).astype(np.float32)
@@ -469,8 +520,74 @@ def seeded_state_dict(seed: int = 20261016, dvc_seed: int = 20261015):
     return sd
 
 
-def get_rlvc_model(seed: int = 20261016, device="cuda"):
+# Entries of a reference RLVC state_dict that load_state_dict_all itself skips (models.py:446-448):
+# the coder tables, rebuilt by update().
+_SKIPPED_SUFFIXES = ("._offset", "._quantized_cdf", "._cdf_length", ".scale_table")
+
+
+def _derived_buffers():
+    """compressai 1.2.x constant buffers a reference RLVC state_dict carries and this build derives
+    from the same constructor constants instead of storing (restated from compressai's published
+    source, which is not importable here -- SURVEY §8(c)): GDN's NonNegativeParametrizer
+    (pedestal 2^-36, LowerBound sqrt(minimum + pedestal), beta_min 1e-6), EntropyBottleneck.target
+    (tail_mass 1e-9), EntropyModel's likelihood LowerBound (1e-9), GaussianConditional's scale
+    bound (0.11). Suffix -> expected value."""
+    ped = 2.0 ** -36
+    t = float(np.log(2 / 1e-9 - 1))
+    return {
+        "beta_reparam.pedestal": [ped], "beta_reparam.lower_bound.bound": [(1e-6 + ped) ** 0.5],
+        "gamma_reparam.pedestal": [ped], "gamma_reparam.lower_bound.bound": [ped ** 0.5],
+        "entropy_bottleneck.entropy_bottleneck.target": [-t, 0.0, t],
+        "likelihood_lower_bound.bound": [1e-9],
+        "gaussian_conditional.scale_bound": [0.11], "gaussian_conditional.lower_bound_scale.bound": [0.11],
+    }
+
+
+def load_state_dict_all(model, state_dict):
+    """models.py:444-449: copy every entry of a reference state_dict into the model, skipping the
+    coder tables. Like the reference, an entry the model does not have raises KeyError and a
+    shape mismatch raises; compressai's derived constant buffers (``_derived_buffers``) are
+    checked against their constants instead of stored. Returns the model's keys that the
+    state_dict did not set."""
+    own = model.state_dict()
+    derived = _derived_buffers()
+    seen = set()
+    for name, param in state_dict.items():
+        if name.endswith(_SKIPPED_SUFFIXES):
+            continue
+        param = torch.as_tensor(param)
+        if name in own:
+            if tuple(own[name].shape) != tuple(param.shape):
+                raise ValueError(f"{name}: shape {tuple(param.shape)} != {tuple(own[name].shape)}")
+            with torch.no_grad():
+                own[name].copy_(param)
+            seen.add(name)
+            continue
+        suffix = next((k for k in derived if name.endswith("." + k)), None)
+        if suffix is None:
+            raise KeyError(name)
+        want = torch.tensor(derived[suffix], dtype=torch.float64)
+        got = param.detach().double().reshape(-1).cpu()
+        if got.shape != want.shape or not torch.allclose(got, want, rtol=1e-5, atol=0.0):
+            raise ValueError(f"{name}: {got.tolist()} differs from compressai's constant {want.tolist()}")
+    model.invalidate()
+    return sorted(set(own) - seen)
+
+
+def get_rlvc_model(seed: int = 20261016, device="cuda", checkpoint=None):
+    """RLVC with seeded weights, or a reference checkpoint: a path (``torch.load`` with
+    ``weights_only=True``), a state_dict, or a dict holding one under 'state_dict' -- loaded with
+    the reference's ``load_state_dict_all`` semantics (models.py:444-449)."""
     m = RLVC()
+    if checkpoint is not None:
+        ck = checkpoint
+        if isinstance(ck, (str, bytes, os.PathLike)):
+            ck = torch.load(ck, map_location="cpu", weights_only=True)
+        if isinstance(ck, dict) and "state_dict" in ck and isinstance(ck["state_dict"], dict):
+            ck = ck["state_dict"]
+        m.missing_checkpoint_keys = load_state_dict_all(m, ck)
+        m.weights_source = "checkpoint"
+        return m.to(device).eval()
     sd = {k: torch.from_numpy(np.ascontiguousarray(v)) for k, v in seeded_state_dict(seed).items()}
     missing, unexpected = m.load_state_dict(sd, strict=False)
     if unexpected:
@@ -478,4 +595,5 @@ def get_rlvc_model(seed: int = 20261016, device="cuda"):
     bad = [k for k in missing if not k.endswith(("weight", "bias")) or "dec_lstm" not in k]
     if bad:
         raise KeyError(f"missing keys {bad[:5]}")
+    m.weights_source = "seeded"
     return m.to(device).eval()

@@ -87,9 +87,42 @@ def refidx_from_graph(g, bs):
     return ref_index
 
 
-def coding_layers(bs, isLinear=False, isOnehop=False):
-    """The layers of graph_from_batch(bs) restricted to frames 1..bs, with each frame's parent."""
-    _, layers, parents = graph_from_batch(bs, isLinear, isOnehop)
+def binary_tree_graph(depth):
+    """The reference's tree shape generalised: P-frames 1..2^depth - 2 as a complete binary tree
+    in pre-order under the I-frame, children of node k at k + 1 and k + 1 + (size of k's left
+    subtree). depth 2..5 give exactly generate_graph('2layers' .. '5layers') (tests/
+    test_tree_gop.py); depth 6 (62 frames) is this build's extension for GOPs past the
+    reference's 30-frame limit (graph_from_batch raises there, as the reference fails)."""
+    if depth < 2:
+        raise ValueError("depth >= 2")
+    g, parents, layers = {}, {}, []
+
+    def build(k, level, size):  # node k at tree level `level` (0 = I-frame) heads `size` nodes
+        if size <= 1:
+            return
+        half = (size - 1) // 2  # nodes under each child
+        kids = [k + 1, k + 1 + half]
+        g[k] = kids
+        while len(layers) <= level:
+            layers.append([])
+        for c in kids:
+            parents[c] = k
+            layers[level].append(c)
+            build(c, level + 1, half)
+
+    build(0, 0, 2 ** depth - 1)
+    return g, [sorted(l) for l in layers], parents
+
+
+def coding_layers(bs, isLinear=False, isOnehop=False, extend=False):
+    """The layers of graph_from_batch(bs) restricted to frames 1..bs, with each frame's parent.
+    extend=True: past the reference's 30 frames, the 62-frame binary tree (binary_tree_graph)."""
+    if extend and bs > 30 and not (isLinear or isOnehop):
+        if bs > 62:
+            raise ValueError(f"Batch size not supported yet: {bs}")
+        _, layers, parents = binary_tree_graph(6)
+    else:
+        _, layers, parents = graph_from_batch(bs, isLinear, isOnehop)
     out = []
     for layer in layers:
         tl = [t for t in layer if t <= bs]
@@ -99,30 +132,36 @@ def coding_layers(bs, isLinear=False, isOnehop=False):
 
 
 def encode_decode_tree_gop(model, frames: torch.Tensor, check=False, overlap=True, isLinear=False,
-                           isOnehop=False):
+                           isOnehop=False, join=True, extend=False):
     """frames: [G, T, 3, H, W] device tensor (frame 0 of each GOP is the I-frame, passed through).
     Codes the T-1 P-frames of every GOP layer by layer: one encoder forward per layer over all
     G x len(layer) frames, then range coding, entropy decoding and reconstruction of that layer
     on side streams (as gop.encode_decode_gop). Returns (bitstreams, decoded, sses, enc_recons):
     bitstreams[i] is the PFrameBitstream of layer i with batch order (frame-major: frame j of the
     layer, GOP g at j*G + g); decoded / enc_recons map P-frame index t to its [G,3,H,W] recon;
-    sses[i] are layer i's encoder SSE sums (device doubles). All results are joined to the
-    caller's stream. A split-precision overflow in any layer re-codes the GOP on the fp32
-    kernels (model.on_overflow == "recompute") or raises FvcError."""
+    sses[i] are layer i's encoder SSE sums (device doubles). With join=True all results are
+    joined to the caller's stream and a split-precision overflow in any layer re-codes the GOP on
+    the fp32 kernels (model.on_overflow == "recompute") or raises FvcError. join=False
+    (streaming, bench.py's timed loop, as gop.encode_decode_gop): no host wait and no join; the
+    overflow probes stay on the model for gop.check_overflow after the caller synchronises."""
+    if not join:
+        if not hasattr(model, "_overflow_probes"):
+            model._overflow_probes = []
+        return _tree(model, frames, check, overlap, isLinear, isOnehop, model._overflow_probes, join, extend)
     probes = []
-    out = _tree(model, frames, check, overlap, isLinear, isOnehop, probes)
+    out = _tree(model, frames, check, overlap, isLinear, isOnehop, probes, join, extend)
     if probes and any(p.result() for p in probes):
         model.overflow_events = getattr(model, "overflow_events", 0) + 1
         if model.on_overflow == "raise":
             raise _lib.FvcError("split-precision conv operand overflow in a tree GOP")
         with K.precision("f32"):
-            return _tree(model, frames, check, overlap, isLinear, isOnehop, [])
+            return _tree(model, frames, check, overlap, isLinear, isOnehop, [], join, extend)
     return out
 
 
-def _tree(model, frames, check, overlap, isLinear, isOnehop, probes):
+def _tree(model, frames, check, overlap, isLinear, isOnehop, probes, join=True, extend=False):
     G, T = frames.shape[:2]
-    lay = coding_layers(T - 1, isLinear, isOnehop)
+    lay = coding_layers(T - 1, isLinear, isOnehop, extend)
     main = torch.cuda.current_stream(frames.device)
     if overlap:
         s_cd0, s_cd1, s_rec = _side_streams(frames.device)
@@ -154,14 +193,19 @@ def _tree(model, frames, check, overlap, isLinear, isOnehop, probes):
                 ref_d = torch.cat([dec[p] for _, p in layer], 0).contiguous()
                 rec = model.reconstruct(dlat, ref_d)
             if overlap:
+                if i == 0 and not join:
+                    _record(enc[0], s_rec)  # the I-frames: decoder references of layer 0
                 _record(lat, s_cd)
                 _record(dlat, s_rec)
+                if not join:
+                    _record(ref_d, s_rec)
             for j, (t, _) in enumerate(layer):
                 enc[t] = clipped[j * G:(j + 1) * G]
                 dec[t] = rec[j * G:(j + 1) * G]
             bitstreams.append(bs)
             sses.append(sse)
-    join_side_streams(frames.device)
+    if join:
+        join_side_streams(frames.device)
     decoded = {t: v for t, v in dec.items() if t > 0}
     enc_recons = {t: v for t, v in enc.items() if t > 0}
     return bitstreams, decoded, sses, enc_recons

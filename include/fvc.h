@@ -188,10 +188,12 @@ int fvc_gdn_tap_nhwc(const float* x, float* P, const float* beta, const float* g
  * Deterministic (fixed-order, no atomics) two-pass reductions; ws must hold
  * fvc_reduce_ws_doubles() doubles. Results are written to device doubles. */
 size_t fvc_reduce_ws_doubles(void);
-/* clipped = clamp(recon,0,1) as NCHW [b][3][h][w]; out3 = {sum (recon-in)^2, sum (warp-in)^2,
- * sum (pred-in)^2} over b*3*h*w elements (all inputs NHWC cp=4) */
+/* clipped = clamp(recon,0,1) as NCHW [b][3][h][w]; out4 = {sum (recon-in)^2, sum (warp-in)^2,
+ * sum (pred-in)^2, sum (clipped-in)^2} over b*3*h*w elements (all inputs NHWC cp=4): DVC's
+ * mse/warp/inter losses use the unclipped recon (net.py:103-116), RLVC's img_loss / PSNR the
+ * clipped Y1_com (models.py:1019,1033-1034) */
 int fvc_recon_finalize(const float* recon, const float* input, const float* warpframe,
-                       const float* prediction, float* clipped_nchw, double* out3, double* ws,
+                       const float* prediction, float* clipped_nchw, double* out4, double* ws,
                        int batch, int h, int w, fvc_stream_t stream);
 /* bits of round(feature) under Laplace(0, clamp(sigma,1e-5,1e10)) (net.py:121-151) */
 int fvc_bits_laplace(const float* feature, const float* sigma, double* out1, double* ws,

@@ -205,7 +205,8 @@ class CRef:
             path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "build", "librans_ref.so")
             if not os.path.exists(path):
                 import subprocess
-                subprocess.run(["make", "-s", "-C", os.path.dirname(path) + "/.."], check=True)
+                # oracle/build/ does not exist in a fresh clone: run make in oracle/ itself
+                subprocess.run(["make", "-s", "-C", os.path.dirname(os.path.dirname(path))], check=True)
             lib = ctypes.CDLL(path)
             vp, ci = ctypes.c_void_p, ctypes.c_int
             lib.ref_pmf_to_quantized_cdf.argtypes = [vp, ci, ci, vp]

@@ -87,6 +87,14 @@ def eb_forward(sd, prefix, x):
     return back(outputs), back(lik)
 
 
+def eb_aux_loss(sd, prefix, tail_mass=1e-9):
+    """compressai EntropyBottleneck.loss(): sum |logits_cumulative(quantiles) - (-t, 0, t)|,
+    t = log(2 / tail_mass - 1) (called by RecProbModel.loss, entropy_models.py:50-53)."""
+    t = math.log(2 / tail_mass - 1)
+    logits = eb_logits(sd, prefix, sd[f"{prefix}.quantiles"])
+    return torch.abs(logits - torch.tensor([-t, 0.0, t])).sum()
+
+
 def gc_forward(x, scales, means):
     outputs = torch.round(x - means) + means
     values = torch.abs(outputs - means)
@@ -112,14 +120,24 @@ def rec_prob_model(sd, prefix, x, rpm_hidden, RPM_flag, prior_latent):
     return x_hat, lik, rpm_hidden, torch.round(x), sigma, mu
 
 
+def coder2d_decode(sd, prefix, latent_hat, state_dec, padding):
+    """Coder2D's synthesis half (models.py:655-664): deconv + IGDN x3 with the recurrent cell
+    (enc_lstm, models.py:661) after the second, then deconv4 -> (hat, new decoder state)."""
+    deconv = lambda i, v: F.conv_transpose2d(v, sd[f"{prefix}.dec_conv{i}.weight"], sd[f"{prefix}.dec_conv{i}.bias"],
+                                             2, padding, 1)
+    x = gdn_cai(sd, f"{prefix}.igdn1", deconv(1, latent_hat), True)
+    x = gdn_cai(sd, f"{prefix}.igdn2", deconv(2, x), True)
+    x, state_dec = conv_lstm(sd, f"{prefix}.enc_lstm", x, state_dec)  # models.py:661: enc_lstm
+    x = gdn_cai(sd, f"{prefix}.igdn3", deconv(3, x), True)
+    return deconv(4, x), state_dec
+
+
 def coder2d(sd, prefix, x, rae_hidden, rpm_hidden, RPM_flag, prior_latent, padding):
     """Coder2D.forward (eval, 'RLVC'); returns a dict of outputs and intermediates."""
     C = rae_hidden.shape[1] // 4
     state_enc, state_dec = torch.split(rae_hidden, 2 * C, dim=1)
     conv = lambda i, v: F.conv2d(v, sd[f"{prefix}.enc_conv{i}.weight"], sd.get(f"{prefix}.enc_conv{i}.bias"), 2,
                                  padding)
-    deconv = lambda i, v: F.conv_transpose2d(v, sd[f"{prefix}.dec_conv{i}.weight"], sd[f"{prefix}.dec_conv{i}.bias"],
-                                             2, padding, 1)
     x = gdn_cai(sd, f"{prefix}.gdn1", conv(1, x), False)
     x = gdn_cai(sd, f"{prefix}.gdn2", conv(2, x), False)
     x, state_enc = conv_lstm(sd, f"{prefix}.enc_lstm", x, state_enc)
@@ -128,14 +146,11 @@ def coder2d(sd, prefix, x, rae_hidden, rpm_hidden, RPM_flag, prior_latent, paddi
     latent_hat, lik, rpm_hidden, prior_latent, sigma, mu = rec_prob_model(
         sd, f"{prefix}.entropy_bottleneck", latent, rpm_hidden, RPM_flag, prior_latent)
     bits_est = estimate_bits(lik)
-    x = gdn_cai(sd, f"{prefix}.igdn1", deconv(1, latent_hat), True)
-    x = gdn_cai(sd, f"{prefix}.igdn2", deconv(2, x), True)
-    x, state_dec = conv_lstm(sd, f"{prefix}.enc_lstm", x, state_dec)  # models.py:661: enc_lstm
-    x = gdn_cai(sd, f"{prefix}.igdn3", deconv(3, x), True)
-    hat = deconv(4, x)
+    hat, state_dec = coder2d_decode(sd, prefix, latent_hat, state_dec, padding)
+    aux = torch.zeros(()) if RPM_flag else eb_aux_loss(sd, f"{prefix}.entropy_bottleneck.entropy_bottleneck")
     return dict(hat=hat, rae_hidden=torch.cat((state_enc, state_dec), 1), rpm_hidden=rpm_hidden,
                 bits_est=bits_est, prior_latent=prior_latent, latent=latent, latent_hat=latent_hat,
-                sigma=sigma, mu=mu)
+                sigma=sigma, mu=mu, aux=aux)
 
 
 def init_hidden(h, w, C=128, batch=1):
@@ -157,6 +172,7 @@ def forward(sd, Y0_com, Y1_raw, hidden, RPM_flag, mv_prior_latent, res_prior_lat
     bpp_est = (m["bits_est"] + r["bits_est"]) / (H * W * B)
     img_loss = torch.mean((Y1_raw - Y1_com) ** 2)
     psnr = 10.0 * torch.log(1 / img_loss) / math.log(10.0)
+    aux_loss = m["aux"] + r["aux"] / 2  # models.py:1030-1031, stage 'REC'
     return dict(Y1_com=Y1_com, hidden=(m["rae_hidden"], r["rae_hidden"], m["rpm_hidden"], r["rpm_hidden"]),
-                bpp_est=bpp_est, img_loss=img_loss, psnr=psnr, mv_prior_latent=m["prior_latent"],
+                bpp_est=bpp_est, img_loss=img_loss, psnr=psnr, aux_loss=aux_loss, mv_prior_latent=m["prior_latent"],
                 res_prior_latent=r["prior_latent"], mv=mv, mv_hat=m["hat"], Y1_MC=Y1_MC, mv_codec=m, res_codec=r)

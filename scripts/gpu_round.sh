@@ -10,7 +10,7 @@ rc=$?
 echo "pytest exit $rc" >> gpurun_out/pytest_gpu_$TAG.log
 grep -E "passed|failed|error" gpurun_out/pytest_gpu_$TAG.log | tail -5
 [ $rc -le 1 ] || exit $rc
-timeout -k 10 420 python -u bench.py --json-out gpurun_out/bench_$TAG.json > gpurun_out/bench_$TAG.log 2>&1
+timeout -k 10 600 python -u bench.py --json-out gpurun_out/bench_$TAG.json > gpurun_out/bench_$TAG.log 2>&1
 rc2=$?
 echo "bench exit $rc2"; tail -c 600 gpurun_out/bench_$TAG.log
 exit $(( rc > rc2 ? rc : rc2 ))

@@ -88,3 +88,43 @@ def test_bench_run_rank_gloo_ws2():
     assert q_["bitstreams_gathered_to_rank0_bytes"] == sum(100 + g for g in range(4))
     assert q_["psnr_db_mean"] == 30.5
     assert res["metric"].startswith("128x64 ")       # non-1080p runs say so in the metric
+
+
+def _run_bench_cli(argv, tmp_path):
+    import bench
+    out = tmp_path / "line.json"
+    rc = bench.main(argv + ["--dry-run", "--json-out", str(out)])
+    assert rc == 0
+    return json.loads(out.read_text())
+
+
+def test_bench_gpus2_spawns_two_ranks(tmp_path):
+    """`bench.py --gpus 2` with no launcher starts two rank processes itself (gloo host rehearsal
+    job): the result line is labelled n_gpus 2 and covers both ranks' GOPs."""
+    res = _run_bench_cli(["--gpus", "2", "--steps", "2", "--warmup", "1", "--gops-per-gpu", "3",
+                          "--height", "64", "--width", "128", "--gop", "4"], tmp_path)
+    assert res["n_gpus"] == 2 and res["config"]["parallelism"] == "gop-shard x2"
+    assert res["shards"] == {"unit": "gop", "by_rank": [[0, 2, 4], [1, 3, 5]]}
+    assert res["config"]["gops_per_gpu"] == 3
+    assert res["quality"]["bitstreams_gathered_to_rank0_bytes"] == sum(100 + g for g in range(6))
+    dt = 2 * 6 * 3 / res["value"]                   # 6 GOPs x 3 P-frames per step
+    assert dt >= 2 * 0.010 * 0.9                    # rank 1's 10 ms steps bound the time
+
+
+def test_bench_views8_gpus8_view_v_on_rank_v(tmp_path):
+    """BASELINE configs[4]: `--views 8 --gpus 8` puts view v on rank v."""
+    res = _run_bench_cli(["--gpus", "8", "--views", "8", "--steps", "1", "--warmup", "0",
+                          "--height", "64", "--width", "128", "--gop", "3"], tmp_path)
+    assert res["n_gpus"] == 8 and res["config"]["parallelism"] == "view-shard x8"
+    assert res["shards"] == {"unit": "view", "by_rank": [[v] for v in range(8)]}
+    assert res["config"]["views_per_gpu"] == 1
+
+
+def test_bench_refuses_gpus_mismatch_under_launcher(monkeypatch):
+    """Under torchrun (WORLD_SIZE set) a --gpus that disagrees is refused rather than mislabelled."""
+    import pytest
+    import bench
+    monkeypatch.setenv("WORLD_SIZE", "1")
+    monkeypatch.setenv("RANK", "0")
+    with pytest.raises(SystemExit, match="--gpus 2 != WORLD_SIZE 1"):
+        bench.main(["--gpus", "2", "--dry-run"])

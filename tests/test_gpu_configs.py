@@ -84,3 +84,54 @@ def test_4k_gop_batch_split_pipeline(dev):
     torch.cuda.synchronize()
     for a, b, c in zip(dec, enc, dec1):
         assert torch.equal(a, b) and torch.equal(a[1:2], c)
+
+
+def test_views8_1080p_config4(dev):
+    """BASELINE configs[4] at its own size: 8 camera views of 1920x1080 (padded to 1088) batched
+    through the bench's rank job (GOP-3 per view). Decoder recon == encoder recon bit for bit,
+    views 0 and 7 coded alone equal their batch slots, no split-precision overflow, and view 0's
+    frame-1 latents from the 8-view batched forward match the CPU oracle within the 1080p T3
+    bounds (test_gpu_forward.py: aggregate flips <= 1.56e-5 of 1.86 M symbols, dPSNR <= 1e-4 dB)."""
+    import os
+
+    import bench
+    from fastvideocodec_amd import kernels as K
+    from fastvideocodec_amd.gop import encode_decode_gop
+    from fastvideocodec_amd.weights import seeded_torch_state_dict
+    from oracle import dvc_ref
+
+    job = bench.GpuGopJob(_args(views=8, height=1080, width=1920, gop=3), 0, 1, dev)
+    assert job.units == 8 and tuple(job.frames.shape) == (8, 3, 3, 1088, 1920)
+    assert job.shard == list(range(8))
+    K.x3_overflow(reset=True)
+    bss, dec, _, enc = encode_decode_gop(job.model, job.frames, check=True, overlap=True)
+    torch.cuda.synchronize()
+    for a, b in zip(dec, enc):
+        assert torch.equal(a, b)
+    for view in (0, 7):
+        _, dec1, _, enc1 = encode_decode_gop(job.model, job.frames[view:view + 1], check=True, overlap=False)
+        torch.cuda.synchronize()
+        for a, b, c in zip(dec, dec1, enc1):
+            assert torch.equal(a[view:view + 1], b) and torch.equal(b, c)
+    v = job.verify()
+    assert v["bitexact"] and v["overflow_recomputes"] == 0
+    assert not K.x3_overflow(reset=True)
+
+    # view 0, frame 1 (against the I-frame) out of the batched 8-view forward vs the oracle
+    out, t = job.model(job.frames[:, 1].contiguous(), job.frames[:, 0].contiguous(), return_intermediates=True)
+    torch.cuda.synchronize()
+    cur, ref = job.frames[0:1, 1].cpu(), job.frames[0:1, 0].cpu()
+    torch.set_num_threads(min(16, len(os.sched_getaffinity(0))))
+    (o_clip, o_mse, *_), inter = dvc_ref.forward(seeded_torch_state_dict(), cur, ref, return_intermediates=True)
+    nflip = ntot = 0
+    for name, gname, c in (("mvfeature", "quant_mv", 128), ("feature", "compressed_feature", 96),
+                           ("z", "compressed_z", 64)):
+        got = np.round(t[name][0:1, ..., :c].permute(0, 3, 1, 2).cpu().numpy())
+        d = got != inter[gname].numpy()
+        nflip += int(d.sum())
+        ntot += d.size
+    assert nflip / ntot <= 1.56e-5, (nflip, ntot)
+    sse_gpu = float(((out[0][0:1].cpu() - cur) ** 2).sum())
+    sse_cpu = float(((o_clip - cur) ** 2).sum())
+    dpsnr = abs(10 * np.log10(sse_cpu / sse_gpu))
+    assert dpsnr <= 1e-4, dpsnr

@@ -105,6 +105,7 @@ def test_gop_chain_vs_golden(model, dev):
     x_hat, loss, img_loss, be_loss, _, psnr, psnr_list, aux, aux2, _, _ = parallel_compression(None, model, data, False)
     assert x_hat.shape == (3, 3, 256, 256)
     drift = np.abs(np.array(psnr_list) - exp_psnr)
+    print("closed-loop PSNR drift per frame (dB):", drift)
     assert drift[0] <= TOL_PSNR_DB and drift.max() <= 2e-2, drift
     exp_bpp = np.mean([float(g[f"f{i}_bpp"]) for i in range(1, 4)])
     assert abs(be_loss - exp_bpp) <= 1e-2 * exp_bpp
@@ -281,6 +282,7 @@ def oracle_1080p():
 # mv 1.7e-5, feature 1.3e-6, z 0), so a regression to fp16-level accuracy (flip rates ~1e-3) fails.
 TOL_1080P_FLIPS_ALL = 1.56e-5
 TOL_1080P_FLIPS = {"quant_mv": 5e-5, "compressed_feature": 5e-6, "compressed_z": 3.1e-5}
+TOL_1080P_MAX = {"estmv": 1e-4, "warpframe": 3e-3, "prediction": 1e-3}
 
 
 def test_forward_vs_oracle_1080p(model, dev, oracle_1080p):
@@ -296,9 +298,10 @@ def test_forward_vs_oracle_1080p(model, dev, oracle_1080p):
     for name in ("estmv", "warpframe", "prediction"):
         # mean deviation at the small-size tier; the max is a few isolated pixels where SpyNet's
         # warp-and-refine iterations amplify ulp-level differences (the reference itself moves
-        # there between CPU backends) or a flipped MV symbol moves the warp
+        # there between CPU backends) or a flipped MV symbol moves the warp: bounds
+        # ~3x the measured maxima (r2, MI355X: estmv 2.9e-5, warpframe 1.0e-3, prediction 2.8e-4)
         assert report[name + "_mean"] <= 2e-6, report
-        assert report[name] <= 1e-2, report
+        assert report[name] <= TOL_1080P_MAX[name], report
     assert report["dpsnr_db"] <= TOL_PSNR_DB, report
     assert report["bpp_rel"] <= 1e-5, report
 

@@ -452,7 +452,8 @@ def test_recon_finalize(dev):
     r, x, w, p = (torch.rand(2, 3, 16, 24, generator=g) * 1.4 - 0.2 for _ in range(4))
     clipped, sse = K.recon_finalize(*(to_nhwc(t).to(dev) for t in (r, x, w, p)))
     assert torch.equal(clipped.cpu(), r.clamp(0, 1))
-    for i, t in enumerate((r, w, p)):
+    assert sse.shape == (4,)
+    for i, t in enumerate((r, w, p, r.clamp(0, 1))):
         assert abs(float(sse[i]) - float(((t.double() - x.double()) ** 2).sum())) < 1e-9 * float(((t - x) ** 2).sum()) + 1e-6
 
 
