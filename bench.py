@@ -80,6 +80,30 @@ def cpu_cores():
     return n
 
 
+class _Heartbeat:
+    """A progress line on stderr every `every` seconds while a long host-side stage runs (the CPU
+    leg's 1080p runs print nothing for minutes otherwise)."""
+
+    def __init__(self, every=30.0):
+        import threading
+        self.stage, self.every, self.t0 = "start", every, time.perf_counter()
+        self._stop = threading.Event()
+        self._th = threading.Thread(target=self._run, daemon=True)
+
+    def _run(self):
+        while not self._stop.wait(self.every):
+            print(f"[bench] cpu baseline: {self.stage} ({time.perf_counter() - self.t0:.0f} s)", file=sys.stderr,
+                  flush=True)
+
+    def __enter__(self):
+        self._th.start()
+        return self
+
+    def __exit__(self, *exc):
+        self._stop.set()
+        self._th.join()
+
+
 def _median_time(fn, reps):
     ts = []
     for _ in range(reps):
@@ -116,34 +140,40 @@ def cpu_baseline(model, dev, frames_np, mode="quick"):
         dvc_ref.decode(sd, ref, inter["quant_mv"], inter["compressed_z"], inter["compressed_feature"])
         state["out"], state["inter"] = out, inter
 
-    small = make_gop(256, 256, 2, 20261015)
-    c1, r1 = torch.from_numpy(small[1:2].copy()), torch.from_numpy(small[0:1].copy())
-    f256 = lambda: dvc_ref.forward(sd, c1, r1)
-    f256()
-    t_256 = _median_time(f256, 3)[0]
-    torch.set_num_threads(1)
-    f256()
-    t_256_1 = _median_time(f256, 3)[0]
-    torch.set_num_threads(cores)
+    hb = _Heartbeat()
+    with hb:
+        hb.stage = "256x256"
+        small = make_gop(256, 256, 2, 20261015)
+        c1, r1 = torch.from_numpy(small[1:2].copy()), torch.from_numpy(small[0:1].copy())
+        f256 = lambda: dvc_ref.forward(sd, c1, r1)
+        f256()
+        t_256 = _median_time(f256, 3)[0]
+        torch.set_num_threads(1)
+        f256()
+        t_256_1 = _median_time(f256, 3)[0]
+        torch.set_num_threads(cores)
 
-    full = mode == "full"
-    if full:
-        enc_dec()  # warm-up
-    t_1080, runs_1080 = _median_time(enc_dec, 3 if full else 1)
-    one_thread_1080 = None
-    one_thread_note = None
-    if full:
-        # the 1-thread 1080p run is bounded so the default bench stays within a few minutes: its
-        # length is predicted from the all-core 1080p median and the 256x256 thread-scaling ratio
-        est = t_1080 * t_256_1 / max(t_256, 1e-9)
-        if est <= ONE_THREAD_1080_BUDGET_S:
-            torch.set_num_threads(1)
-            one_thread_1080 = _median_time(enc_dec, 1)[0]
-            torch.set_num_threads(cores)
-        else:
-            one_thread_note = f"skipped: predicted {est:.0f} s > {ONE_THREAD_1080_BUDGET_S:.0f} s budget"
+        full = mode == "full"
+        hb.stage = f"1080p on {cores} threads"
+        if full:
+            enc_dec()  # warm-up
+        t_1080, runs_1080 = _median_time(enc_dec, 3 if full else 1)
+        one_thread_1080 = None
+        one_thread_note = None
+        if full:
+            # the 1-thread 1080p run is bounded so the default bench stays within a few minutes: its
+            # length is predicted from the all-core 1080p median and the 256x256 thread-scaling ratio
+            est = t_1080 * t_256_1 / max(t_256, 1e-9)
+            if est <= ONE_THREAD_1080_BUDGET_S:
+                hb.stage = f"1080p on 1 thread (predicted {est:.0f} s)"
+                torch.set_num_threads(1)
+                one_thread_1080 = _median_time(enc_dec, 1)[0]
+                torch.set_num_threads(cores)
+            else:
+                one_thread_note = f"skipped: predicted {est:.0f} s > {ONE_THREAD_1080_BUDGET_S:.0f} s budget"
+        hb.stage = "parity block"
 
-    parity, coder = parity_block(model, dev, cur, ref, state["out"], state["inter"], R)
+        parity, coder = parity_block(model, dev, cur, ref, state["out"], state["inter"], R)
     cpu_model = ""
     try:
         cpu_model = next(l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name"))
@@ -286,7 +316,9 @@ class GpuGopJob:
         with timer:
             encode_decode_gop(self.model, self.frames, overlap=False)
         r = {"conv": timer.collect(), "x3": timer.collect(x3=True), "x3_bytes": timer.collect_bytes(x3=True),
-             "hbm": timer.collect_hbm()}
+             "hbm": timer.collect_hbm(),
+             "family": {f: (timer.collect(x3=True, family=f), timer.collect_bytes(x3=True, family=f))
+                        for f in ("x3", "wino")}}
         if self.args.breakdown:
             for k, (n, ms, fl) in sorted(timer.breakdown().items(), key=lambda kv: -kv[1][1]):
                 print(f"{k:40s} n={n:5d} ms={ms:9.2f} TF/s={fl / (ms * 1e-3) / 1e12:7.2f}", file=sys.stderr)
@@ -437,11 +469,15 @@ def roofline_fields(prof, job, args):
                      "avg_launch_us": round(x3_ms * 1e3 / x3_launch, 2) if x3_launch else None,
                      "algorithmic_bytes_per_launch": round(x3_bytes / x3_launch) if x3_launch else None,
                      "algorithmic_gbps": round(x3_bytes / (x3_ms * 1e-3) / 1e9, 1) if x3_ms else None,
-                     "kernel": "conv_x3_kernel (split-precision fp16x3 implicit-GEMM conv/deconv): all its launches",
-                     "achieved_is": "algorithmic fp32-conv FLOP (2 x MAC) / kernel time; the kernel issues 3 f16 "
-                                    "MFMAs per MAC, so its ceiling in these units is peak/3",
+                     "kernel": "split-precision conv kernels (every conv launch but 4 small-cin layers): "
+                               "conv_x3_kernel (fp16x3 implicit-GEMM conv/deconv) + conv_wino_kernel (Winograd "
+                               "F(2x2,3x3) for the 64->64 3x3 layers), all their launches",
+                     "achieved_is": "algorithmic fp32-conv FLOP (2 x MAC of the direct convolution) / kernel time; "
+                                    "the direct kernel issues 3 f16 MFMAs per MAC (ceiling peak/3), the Winograd "
+                                    "kernel 3 per 16/36 MAC (ceiling peak/3 x 36/16)",
                      "x3_ceiling": round(F16_MFMA_PEAK_TFLOPS / 3, 1),
                      "frac_of_x3_ceiling": round(achieved / (F16_MFMA_PEAK_TFLOPS / 3), 4),
+                     "per_kernel": per_kernel_fields(prof, nfr),
                      "measured": "HIP events on the launching stream around every conv launch of one serial GOP",
                      "launches": x3_launch, "ms_per_pframe": round(x3_ms / nfr, 3),
                      "gflop_per_pframe": round(x3_flops / nfr / 1e9, 1),
@@ -457,12 +493,30 @@ def roofline_fields(prof, job, args):
     }
 
 
+def per_kernel_fields(prof, nfr):
+    """The roofline object split by kernel: algorithmic TF/s, launches and time of conv_x3_kernel
+    and conv_wino_kernel, and for Winograd the f16 matrix rate it actually issues (3 MFMAs per
+    16/36 of a direct MAC)."""
+    out = {}
+    for fam, name, mac_frac in (("x3", "conv_x3_kernel", 1.0), ("wino", "conv_wino_kernel", 16.0 / 36.0)):
+        (ms, fl, n), nbytes = prof["family"][fam]
+        if not n:
+            continue
+        tf = fl / (ms * 1e-3) / 1e12
+        out[name] = {"achieved": round(tf, 2), "launches": n, "avg_launch_us": round(ms * 1e3 / n, 2),
+                     "ms_per_pframe": round(ms / nfr, 3), "gflop_per_pframe": round(fl / nfr / 1e9, 1),
+                     "algorithmic_gbps": round(nbytes / (ms * 1e-3) / 1e9, 1),
+                     "f16_mfma_tflops_issued": round(3 * mac_frac * tf, 1),
+                     "frac_of_f16_peak_issued": round(3 * mac_frac * tf / F16_MFMA_PEAK_TFLOPS, 4)}
+    return out
+
+
 def load_pmc_traffic(H, W):
     """HBM bytes per conv_x3_kernel launch from the committed rocprofv3 FETCH_SIZE/WRITE_SIZE passes
     over `bench.py --serial` (profiles/<round>/x3_traffic.json, written by scripts/rocprof_summary.py;
     FETCH_SIZE doubled per MI355X_MICROARCH.md's gfx950 correction). PMC passes serialise every
     dispatch and cannot run inside the timed region, so the figure is the profiled one."""
-    for rnd in ("r2", "r1"):
+    for rnd in ("r3", "r2", "r1"):
         path = os.path.join(REPO, "profiles", rnd, "x3_traffic.json")
         try:
             with open(path) as f:

@@ -38,6 +38,10 @@ _SIGS = {
                                + [c_int] * 2 + [vp, vp, c_int, vp]),
     "fvc_deconv2d_nhwc_x3_tap": (c_int, [vp, vp, c_float, vp, vp, vp] + [c_int] * 8 + [vp, c_float]
                                  + [c_int] * 2 + [vp, vp, c_int, vp]),
+    "fvc_conv_wino_supported": (c_int, [c_int] * 5),
+    "fvc_conv_wino_wpack_bytes": (c_size_t, []),
+    "fvc_conv_wino_pack_weight": (c_int, [vp, vp, vp]),
+    "fvc_conv2d_nhwc_wino": (c_int, [vp, vp, c_float, vp, vp, vp, vp] + [c_int] * 6 + [vp, vp, c_int, vp]),
     "fvc_nchw_to_nhwc": (c_int, [vp, vp, c_int, c_int, c_int, c_int, c_int, vp]),
     "fvc_nhwc_to_nchw": (c_int, [vp, vp, c_int, c_int, c_int, c_int, c_int, c_int, vp]),
     "fvc_avgpool2_nhwc": (c_int, [vp, vp, c_int, c_int, c_int, c_int, vp]),

@@ -11,7 +11,10 @@ from concurrent.futures import ThreadPoolExecutor
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 VARIANT_SRCS = ("fvc_conv_x3.hip",)
-SRCS = ["fvc_conv.hip", "fvc_conv_x3.hip", "fvc_elem.hip", "fvc_coder.hip", "fvc_iframe.hip", "fvc_torchac.hip"]
+SRCS = ["fvc_conv.hip", "fvc_conv_x3.hip", "fvc_conv_wino.hip", "fvc_elem.hip", "fvc_coder.hip", "fvc_iframe.hip",
+        "fvc_torchac.hip"]
+# per-source flags: the Winograd transforms stay scalar f32 (packed f32 VALU issues slower beside MFMAs)
+SRC_FLAGS = {"fvc_conv_wino.hip": ["-fno-slp-vectorize"]}
 OUT = os.path.join(HERE, "libfvc.so")
 OBJDIR = os.path.join(HERE, "build")
 HEADERS = [os.path.join(HERE, "csrc", "fvc_common.h"), os.path.join(HERE, "csrc", "fvc_dist.h"),
@@ -37,7 +40,7 @@ def _stale(target, deps):
 def _compile(src, verbose, extra=(), tag=""):
     path = os.path.join(HERE, "csrc", src)
     obj = _obj(src, tag)
-    cmd = [_hipcc()] + FLAGS + list(extra) + ["-c", path, "-o", obj + ".tmp"]
+    cmd = [_hipcc()] + FLAGS + SRC_FLAGS.get(src, []) + list(extra) + ["-c", path, "-o", obj + ".tmp"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)

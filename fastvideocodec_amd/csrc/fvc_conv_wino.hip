@@ -1,0 +1,634 @@
+// Winograd F(2x2, 3x3) split-precision convolution for the 64 -> 64-channel, 3x3, stride-1 layers
+// (Warp_net's ResBlocks, DVC/subnet/endecoder.py:228-296) on the fp16 matrix cores
+// (v_mfma_f32_16x16x32_f16), at fp32-level accuracy. Replaces the same ATen conv2d calls as
+// fvc_conv_x3.hip for that geometry: 16 products per (2x2 output tile, channel pair) instead of 36,
+// i.e. 2.25x fewer matrix instructions for the same algorithmic work.
+//
+// Algorithm (Lavin & Gray 2016): for each 2x2 output tile the 4x4 input patch d is transformed,
+// V = B^T d B; every transformed position p is an independent GEMM over the input channels with the
+// transformed weights U[p] = (G g G^T)[p]: M[p] = sum_c U[p][c] V[p][c]; the tile is Y = A^T M A,
+// then bias, activation and residual as the direct kernel. F(2,3) matrices:
+//   B^T rows (1,0,-1,0) (0,1,1,0) (0,-1,1,0) (0,1,0,-1)   (input: additions only)
+//   G   rows (1,0,0) (1/2,1/2,1/2) (1/2,-1/2,1/2) (0,0,1) (weights, on the host in double)
+//   A^T rows (1,1,1,0) (0,1,-1,-1)                        (output: additions only)
+//
+// Numerics as fvc_conv_x3.hip: U (scaled by 2^kw so max|U| is in [2^13, 2^14)) and V (fp32 here)
+// are split exactly into fp16 hi + lo * 2^-11; main += U_hi V_hi and corr += U_lo V_hi + U_hi V_lo
+// in two fp32 accumulators. |V| <= 4 max|x|: a transformed value >= 65000 (or NaN) sets the
+// caller's overflow flag (the host then recomputes on the fp32 kernels).
+//
+// Resident weights: one 256-thread block per CU, one wave per SIMD with 512 registers. Wave r owns
+// row r of the 4x4 transform domain (positions (r, q), q = 0..3) for all 64 output channels: its
+// 64 KB of U (hi and lo planes) is loaded once per launch and stays in registers, so the k-loop
+// reads no weights at all. A work item is a row of 16 tiles (2 output rows x 32 columns); per item
+// each lane transforms the input of its tile (lane & 15) and 8 channels straight into the MFMA B
+// operand of its wave's 4 positions (no V in memory). The waves then exchange the column-combined
+// partial results Z[r][j] = sum_q M[r][q] A[q][j] through LDS (double-buffered: one barrier per
+// item) and wave w finishes output channels 16w .. 16w+15: Y[i][j] = sum_r A^T[i][r] Z[r][j].
+// Input: a ring of 8 raw fp32 input rows in LDS filled by LDS-DMA (global_load_lds_dwordx4, a zero
+// page for the padding); consecutive items of a block walk down one tile column, so each item
+// stages the 2 new rows of its 4-row window while the previous item computes.
+// LDS input layout: row slot -> 16 channel quads -> 40 column slots of 16 B, even columns 0..16 then
+// odd columns 17..33 (the tile columns of a patch are 2 apart): a lane group's ds_read_b128 of 16
+// tiles x 2 octets covers all 64 banks once.
+// Epilogue forms: plain (bias, ReLU / LeakyReLU, residual add), and POOL, which also writes the
+// 2x2 average pool of the output (each pool window is one Winograd tile: ATen's ((x00 + x01) + x10)
+// + x11) / 4, bit-identical to k_avgpool2).
+#include "fvc_common.h"
+#include <math.h>
+#include <stdlib.h>
+
+namespace {
+
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f2v __attribute__((ext_vector_type(2)));
+typedef _Float16 h2v __attribute__((ext_vector_type(2)));
+typedef unsigned v4u __attribute__((ext_vector_type(4)));
+
+constexpr int kC = 64;             // input and output channels
+constexpr int kQ = kC / 4;         // channel quads per pixel
+constexpr int kTiles = 16;         // tiles per item: one tile row x 16 tile columns
+constexpr int kCols = 2 * kTiles + 2;  // input columns an item reads
+constexpr int kSlots = 40;         // column slots per (row, quad) line (34 used)
+constexpr int kRowEntries = kQ * kSlots;   // 16-B entries per staged row (640)
+constexpr int kRing = 8;           // staged input rows
+constexpr int kRingBytes = kRing * kRowEntries * 16;  // 81920
+constexpr int kZBytes = 4 * 8 * 1024;                 // one Z buffer: 4 waves x 8 planes x 1 KB
+constexpr int kHdr = 512;                             // bias (256 B) + schedule words
+constexpr int kLds = kHdr + kRingBytes + 2 * kZBytes; // 148,480 B
+constexpr int kChunk = 16;         // items per schedule chunk (consecutive tile rows of one column)
+constexpr float kLoScale = 2048.f;
+constexpr unsigned kOob = 0xFFFFFF00u;
+constexpr int kRsrcFlags = 0x00020000;
+constexpr int kPostPool = 1;
+
+__device__ __attribute__((aligned(16))) float g_wino_zero[4];  // zero page for padding pixels
+
+struct WinoArgs {
+  const float* x;
+  const uint4* u;        // packed U: [wave r][q][n][kk][plane][lane] 16-B fragments
+  const float* bias;
+  const float* res;
+  float* y;
+  float* pool;
+  int B, H, W;
+  int tiles_y, ngroups;  // tile rows, 32-column groups
+  int nchunks, chunks_per_col;
+  float osc, osc_c;      // 2^-kw, 2^-kw-11
+  unsigned y_bytes, res_bytes, pool_bytes, x_bytes;
+  int* sched;            // [0] blocks finished, [1] next chunk; zero on entry, reset by the last block
+  int* ovf;
+};
+
+__device__ __forceinline__ unsigned lds_addr(const void* p) {
+  return __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)((const __attribute__((address_space(3))) char*)p));
+}
+
+// One 1-KB LDS-DMA piece: lane l's 16 B at g land at LDS byte lds + 16 l (M0 saved and restored;
+// the kernel drains these itself with vmcnt(0) before the barrier that publishes the rows).
+__device__ __forceinline__ void glds16(const void* g, unsigned lds) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(g), "s"(lds)
+               : "memory");
+}
+
+// v = hi + lo * 2^-11 for 8 values; mx tracks max |v|. Scalar f32 arithmetic: packed f32 VALU
+// (v_pk_*_f32) issues slower than two plain ops beside MFMAs (MI355X_MICROARCH.md, fillers).
+__device__ __forceinline__ void split8(const float (&v)[8], h8& hi, h8& lo, float& mx) {
+#pragma unroll
+  for (int i = 0; i < 8; i += 2) {
+    const f2v x = {v[i], v[i + 1]};
+    const h2v h = __builtin_convertvector(x, h2v);  // v_cvt_pk_f16_f32 (round to nearest even)
+    const float d0 = (v[i] - (float)h[0]) * kLoScale;
+    const float d1 = (v[i + 1] - (float)h[1]) * kLoScale;
+    const f2v d = {d0, d1};
+    const h2v l = __builtin_convertvector(d, h2v);
+    hi[i] = h[0];
+    hi[i + 1] = h[1];
+    lo[i] = l[0];
+    lo[i + 1] = l[1];
+  }
+  mx = fmaxf(mx, fmaxf(fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))),
+                       fmaxf(fmaxf(fabsf(v[4]), fabsf(v[5])), fmaxf(fabsf(v[6]), fabsf(v[7])))));
+}
+
+// The three split-precision products of one (position, 16-channel N-tile) pair:
+//   acc += U_hi V_hi, cor += U_lo V_hi, cor += U_hi V_lo
+// U is an AGPR operand ("a": the 256 resident U registers fill the accumulator half of the file,
+// the k-loop's VGPRs stay free for the transforms); hipcc does not place MFMAs with A/B operands
+// in AGPRs, hence inline asm. Wait states (cdna_hip_programming.md §5.7): a VALU write of vh / vl
+// or a v_accvgpr_write of U right before -> 2 states (s_nop 1, opening the string); the
+// accumulate chains need none; the VALU reads of acc / cor after the item's last MFMA are fenced
+// by wino_mfma_drain.
+template <bool FIRST>
+__device__ __forceinline__ void wino_mfma3(f32x4& acc, f32x4& cor, const h8& uh, const h8& ul, const h8& vh,
+                                           const h8& vl) {
+  if constexpr (FIRST) {  // first k-step of an item: the chains start from C = 0
+    asm volatile(
+        "s_nop 1\n\t"
+        "v_mfma_f32_16x16x32_f16 %0, %2, %4, 0\n\t"
+        "v_mfma_f32_16x16x32_f16 %1, %3, %4, 0\n\t"
+        "v_mfma_f32_16x16x32_f16 %1, %2, %5, %1"
+        : "=&v"(acc), "=&v"(cor)
+        : "a"(uh), "a"(ul), "v"(vh), "v"(vl));
+  } else {
+    asm volatile(
+        "s_nop 1\n\t"
+        "v_mfma_f32_16x16x32_f16 %0, %2, %4, %0\n\t"
+        "v_mfma_f32_16x16x32_f16 %1, %3, %4, %1\n\t"
+        "v_mfma_f32_16x16x32_f16 %1, %2, %5, %1"
+        : "+v"(acc), "+v"(cor)
+        : "a"(uh), "a"(ul), "v"(vh), "v"(vl));
+  }
+}
+
+// 12 wait states after the last MFMA of an item (the 8-pass XDL bound, cdna_hip_programming.md
+// §5.7 item 2) before any VALU reads an accumulator; the accumulators are operands so no reader is
+// scheduled above it
+__device__ __forceinline__ void wino_mfma_drain(f32x4 (&acc)[4][4], f32x4 (&cor)[4][4]) {
+  asm volatile("s_nop 11" : "+v"(acc[0][0]), "+v"(acc[0][1]), "+v"(acc[0][2]), "+v"(acc[0][3]),
+               "+v"(acc[1][0]), "+v"(acc[1][1]), "+v"(acc[1][2]), "+v"(acc[1][3]));
+  asm volatile("" : "+v"(acc[2][0]), "+v"(acc[2][1]), "+v"(acc[2][2]), "+v"(acc[2][3]), "+v"(acc[3][0]),
+               "+v"(acc[3][1]), "+v"(acc[3][2]), "+v"(acc[3][3]));
+  asm volatile("" : "+v"(cor[0][0]), "+v"(cor[0][1]), "+v"(cor[0][2]), "+v"(cor[0][3]), "+v"(cor[1][0]),
+               "+v"(cor[1][1]), "+v"(cor[1][2]), "+v"(cor[1][3]));
+  asm volatile("" : "+v"(cor[2][0]), "+v"(cor[2][1]), "+v"(cor[2][2]), "+v"(cor[2][3]), "+v"(cor[3][0]),
+               "+v"(cor[3][1]), "+v"(cor[3][2]), "+v"(cor[3][3]));
+}
+
+// max(x, 0) as one v_max_f32 (fmaxf compiles to a NaN-quieting v_max x, x first)
+__device__ __forceinline__ float relu1(float x) {
+  float r;
+  asm("v_max_f32 %0, 0, %1" : "=v"(r) : "v"(x));
+  return r;
+}
+
+// y = hi + lo * 2^-11 for two values: hi by one packed round-to-nearest conversion, the residual
+// y - hi by v_fma_mix (hi read as f16 inside the FMA: exact), lo rounded straight to f16 by
+// v_fma_mix{lo,hi} (5 VALU per pair instead of 8 for convert / convert back / subtract / scale /
+// convert). Pure VALU asm: the hardware interlocks VALU dependencies.
+__device__ __forceinline__ void split2(float v0, float v1, unsigned& hi, unsigned& lo) {
+  float r0, r1;
+  asm volatile(
+      "v_cvt_pk_f16_f32 %0, %3, %4\n\t"
+      "v_fma_mix_f32 %1, %0, -1.0, %3 op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mix_f32 %2, %0, -1.0, %4 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
+      : "=&v"(hi), "=&v"(r0), "=&v"(r1)
+      : "v"(v0), "v"(v1));
+  asm volatile(
+      "v_fma_mixlo_f16 %0, %1, %3, 0\n\t"
+      "v_fma_mixhi_f16 %0, %2, %3, 0"
+      : "=&v"(lo)
+      : "v"(r0), "v"(r1), "s"(kLoScale));
+}
+
+template <int IOP, int POST, bool RES, int ACT>
+__global__ __launch_bounds__(256, 1) void conv_wino_kernel(const WinoArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* const sbias = reinterpret_cast<float*>(smem);
+  int* const sq = reinterpret_cast<int*>(smem + 256);  // [0..1] first chunks, [2..3] chunk after next
+  char* const ring = smem + kHdr;
+  char* const zbuf = ring + kRingBytes;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // = row r of the transform domain
+  const int t = lane & 15;    // tile of this lane (MFMA B column / D column)
+  const int o = lane >> 4;    // channel octet of this lane within a 32-channel k-step
+  const int W = a.W, H = a.H;
+
+  // resident U: u[q][n][kk][plane], 4 registers each (AGPRs: the MFMA asm's "a" operands)
+  h8 u[4][4][2][2];
+  {
+    const uint4* src = a.u + (size_t)wave * (4 * 4 * 2 * 2 * 64) + lane;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int n = 0; n < 4; ++n)
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+          for (int pl = 0; pl < 2; ++pl)
+            u[q][n][kk][pl] = __builtin_bit_cast(h8, src[(((q * 4 + n) * 2 + kk) * 2 + pl) * 64]);
+  }
+  if (tid < kC) sbias[tid] = a.bias[tid];
+
+  // rows of the 4x4 patch this wave's transform row combines: E = d[ra] + sb * d[rb]
+  // (B^T rows (1,0,-1,0) (0,1,1,0) (0,-1,1,0) (0,1,0,-1)), then V[r][.] = E B (x-transform)
+  const int ra = wave == 0 ? 0 : (wave == 2 ? 2 : 1);
+  const int rb = wave == 0 ? 2 : (wave == 1 ? 2 : (wave == 2 ? 1 : 3));
+  const float sb = wave == 1 ? 1.f : -1.f;
+
+  // DMA pieces of a staged row this wave issues (piece k of 10 -> wave k & 3) and the lane's
+  // part of each: local input column (or -1: pad slot) and channel-quad offset
+  int dma_lc[3], dma_ch[3];
+#pragma unroll
+  for (int m = 0; m < 3; ++m) {
+    const int e = (wave + 4 * m) * 64 + lane;
+    const int c4 = e / kSlots, cs = e - c4 * kSlots;
+    dma_lc[m] = cs < 17 ? 2 * cs : (cs < 34 ? 2 * (cs - 17) + 1 : -(1 << 20));
+    dma_ch[m] = 4 * c4;
+  }
+  const int npiece = wave < 2 ? 3 : 2;  // 10 pieces over 4 waves
+  // stage input row iy of image b, column group g into ring slot s
+  auto stage_row = [&](int b, int g, int iy, int s) {
+    const bool row_ok = (unsigned)iy < (unsigned)H;
+    const size_t rowoff = ((size_t)b * H + (row_ok ? iy : 0)) * W;
+#pragma unroll
+    for (int m = 0; m < 3; ++m) {
+      if (m >= npiece) break;
+      const int ix = 32 * g - 1 + dma_lc[m];
+      const bool ok = row_ok && (unsigned)ix < (unsigned)W;
+      const float* src = ok ? a.x + (rowoff + ix) * kC + dma_ch[m] : g_wino_zero;
+      glds16(src, lds_addr(ring + ((size_t)s * kRowEntries + (wave + 4 * m) * 64) * 16));
+    }
+  };
+
+  // ---- schedule: chunks of kChunk consecutive tile rows of one (image, 32-column group)
+  int* const ctr = a.sched ? a.sched + 1 : nullptr;
+  auto take = [&](int k) -> int {  // thread 0: the k-th chunk this block takes
+    if (ctr) return atomicAdd(ctr, 1);
+    return (int)blockIdx.x + k * (int)gridDim.x;
+  };
+  struct Pos {
+    int b, g, ty0, ty1;  // tile rows [ty0, ty1) of column group g of image b; empty = no chunk
+  };
+  auto decode = [&](int ch) -> Pos {  // once per chunk (two scalar divisions)
+    Pos p{0, 0, 0, 0};
+    if (ch < a.nchunks) {
+      const int col = ch / a.chunks_per_col;
+      p.ty0 = (ch - col * a.chunks_per_col) * kChunk;
+      p.ty1 = min(p.ty0 + kChunk, a.tiles_y);
+      p.b = col / a.ngroups;
+      p.g = col - p.b * a.ngroups;
+    }
+    return p;
+  };
+  // the block knows its current and next chunk; the first item of every chunk takes the one
+  // after (thread 0, into LDS word 2 + parity, decoded by everyone after that item's barrier)
+  if (tid == 0) {
+    sq[0] = take(0);
+    sq[1] = take(1);
+  }
+  __syncthreads();
+  Pos cur = decode(sq[0]);
+  Pos nxt = decode(sq[1]);
+  Pos nnp{0, 0, 0, 0};
+  int ntaken = 2;
+
+  const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc((void*)a.y, (short)0, (int)a.y_bytes, kRsrcFlags);
+  const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc((void*)a.res, (short)0, (int)a.res_bytes, kRsrcFlags);
+  const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc((void*)a.pool, (short)0, (int)a.pool_bytes, kRsrcFlags);
+  h2v mxh = {(_Float16)0.f, (_Float16)0.f};  // max |hi| of every split value (overflow check)
+
+  if (cur.ty0 < cur.ty1) {
+    // first item of the block: its whole 4-row window into ring slots 0..3
+    for (int i = 0; i < 4; ++i) stage_row(cur.b, cur.g, 2 * cur.ty0 - 1 + i, i);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int ty = cur.ty0;
+    int base = 0;  // ring slot of the current item's first row
+    int zb = 0;    // Z buffer
+    for (;;) {
+      const bool first = ty == cur.ty0;
+      const bool cont = ty + 1 < cur.ty1;  // the next item continues down this column: 2 new rows
+      const Pos& np = cont ? cur : nxt;
+      const int nty = cont ? ty + 1 : nxt.ty0;
+      const bool nvalid = cont || nxt.ty0 < nxt.ty1;
+      const int nbase = (base + (cont ? 2 : 4)) & (kRing - 1);
+      if (nvalid) {
+        for (int i = cont ? 2 : 0; i < 4; ++i) stage_row(np.b, np.g, 2 * nty - 1 + i, (nbase + i) & (kRing - 1));
+      }
+      if (first && tid == 0) sq[2 + (ntaken & 1)] = take(ntaken);  // chunk after next
+
+      // this lane's 4 output pixels in the finishing pass (channels 16 wave + 4 o .. +3); the
+      // residual is loaded now so its latency hides behind the k-loop
+      const int oy0 = 2 * ty, ox0 = 32 * cur.g + 2 * t;
+      const int cbase = 16 * wave + 4 * o;
+      unsigned off[2][2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int oy = oy0 + i, ox = ox0 + j;
+          const bool ok = oy < H && ox < W;
+          off[i][j] = ok ? ((unsigned)((cur.b * H + oy) * W + ox) * (unsigned)kC + (unsigned)cbase) * 4u : kOob;
+        }
+      f32x4 rv[2][2];
+      if constexpr (RES) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            rv[i][j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rr, off[i][j], 0, 0));
+      }
+
+      // ---- k-loop: 2 steps of 32 input channels, 48 MFMAs each
+      f32x4 acc[4][4], cor[4][4];
+      const char* rowa = ring + (size_t)((base + ra) & (kRing - 1)) * kRowEntries * 16;
+      const char* rowb = ring + (size_t)((base + rb) & (kRing - 1)) * kRowEntries * 16;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        float v[4][8];  // V[r][q] for the 8 channels of this lane
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+          // patch columns 0..3 of tile t: slots t, 17 + t, t + 1, 18 + t (even / odd column halves)
+          const int e0 = ((8 * kk + 2 * o + hh) * kSlots + t) * 16;
+          const float4 a0 = *reinterpret_cast<const float4*>(rowa + e0);
+          const float4 a1 = *reinterpret_cast<const float4*>(rowa + e0 + 17 * 16);
+          const float4 a2 = *reinterpret_cast<const float4*>(rowa + e0 + 16);
+          const float4 a3 = *reinterpret_cast<const float4*>(rowa + e0 + 18 * 16);
+          const float4 b0 = *reinterpret_cast<const float4*>(rowb + e0);
+          const float4 b1 = *reinterpret_cast<const float4*>(rowb + e0 + 17 * 16);
+          const float4 b2 = *reinterpret_cast<const float4*>(rowb + e0 + 16);
+          const float4 b3 = *reinterpret_cast<const float4*>(rowb + e0 + 18 * 16);
+          const float4 da[4] = {a0, a1, a2, a3}, db[4] = {b0, b1, b2, b3};
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            float e[4];
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) {
+              float xa = da[jj][c], xb = db[jj][c];
+              if constexpr (IOP == FVC_IN_RELU) {
+                xa = relu1(xa);
+                xb = relu1(xb);
+              }
+              e[jj] = fmaf(sb, xb, xa);
+            }
+            v[0][4 * hh + c] = e[0] - e[2];
+            v[1][4 * hh + c] = e[1] + e[2];
+            v[2][4 * hh + c] = e[2] - e[1];
+            v[3][4 * hh + c] = e[1] - e[3];
+          }
+        }
+        h8 vh[4], vl[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          unsigned hw[4], lw[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            split2(v[q][2 * i], v[q][2 * i + 1], hw[i], lw[i]);
+            mxh = __builtin_elementwise_max(mxh, __builtin_elementwise_abs(__builtin_bit_cast(h2v, hw[i])));
+          }
+          vh[q] = __builtin_bit_cast(h8, v4u{hw[0], hw[1], hw[2], hw[3]});
+          vl[q] = __builtin_bit_cast(h8, v4u{lw[0], lw[1], lw[2], lw[3]});
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+          for (int n = 0; n < 4; ++n) {
+            if (kk == 0) wino_mfma3<true>(acc[q][n], cor[q][n], u[q][n][kk][0], u[q][n][kk][1], vh[q], vl[q]);
+            else wino_mfma3<false>(acc[q][n], cor[q][n], u[q][n][kk][0], u[q][n][kk][1], vh[q], vl[q]);
+          }
+      }
+      wino_mfma_drain(acc, cor);
+
+      // ---- column combination Z[r][j] = sum_q M[r][q] A[q][j] (M in units of 2^kw: the scale is
+      // applied once on Y) -> LDS plane (r, j, n), lane-linear
+      char* const zw = zbuf + zb * kZBytes;
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        f32x4 z0, z1;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          float m[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) m[q] = fmaf(cor[q][n][c], 1.f / kLoScale, acc[q][n][c]);
+          z0[c] = (m[0] + m[1]) + m[2];
+          z1[c] = (m[1] - m[2]) - m[3];
+        }
+        *reinterpret_cast<f32x4*>(zw + ((wave * 2 + 0) * 4 + n) * 1024 + lane * 16) = z0;
+        *reinterpret_cast<f32x4*>(zw + ((wave * 2 + 1) * 4 + n) * 1024 + lane * 16) = z1;
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA pieces of the next item
+      __syncthreads();
+      if (first) nnp = decode(sq[2 + (ntaken & 1)]);  // published by this item's barrier
+
+      // ---- finishing pass: wave w -> output channels 16w..16w+15 of the item's 16 tiles
+      f32x4 z[4][2];
+#pragma unroll
+      for (int p = 0; p < 4; ++p)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          z[p][j] = *reinterpret_cast<const f32x4*>(zw + ((p * 2 + j) * 4 + wave) * 1024 + lane * 16);
+      const f32x4 bj = *reinterpret_cast<const f32x4*>(sbias + cbase);
+      f32x4 yv[2][2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          f32x4 vv;
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            const float ys = i == 0 ? (z[0][j][c] + z[1][j][c]) + z[2][j][c] : (z[1][j][c] - z[2][j][c]) - z[3][j][c];
+            float tv = fmaf(ys, a.osc, bj[c]);
+            if constexpr (ACT == FVC_ACT_RELU) tv = relu1(tv);
+            if constexpr (ACT == FVC_ACT_LRELU) tv = fmaxf(tv, 0.1f * tv);
+            if constexpr (RES) tv += rv[i][j][c];
+            vv[c] = tv;
+          }
+          yv[i][j] = vv;
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, vv), ry, off[i][j], 0, 0);
+        }
+      if constexpr (POST == kPostPool) {
+        f32x4 pv;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) pv[c] = (((yv[0][0][c] + yv[0][1][c]) + yv[1][0][c]) + yv[1][1][c]) / 4.f;
+        const int Hp = H >> 1, Wp = W >> 1;
+        const int py = ty, px = 16 * cur.g + t;
+        const unsigned po = (py < Hp && px < Wp)
+                                ? ((unsigned)((cur.b * Hp + py) * Wp + px) * (unsigned)kC + (unsigned)cbase) * 4u
+                                : kOob;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, pv), rp, po, 0, 0);
+      }
+
+      // ---- advance
+      if (!nvalid) break;
+      if (!cont) {
+        cur = nxt;
+        nxt = nnp;
+        ++ntaken;
+      }
+      ty = nty;
+      base = nbase;
+      zb ^= 1;
+    }
+  }
+  {
+    const float mx = fmaxf((float)mxh[0], (float)mxh[1]);
+    if (!(mx < 65000.f) && a.ovf) atomicOr(a.ovf, 1);
+  }
+  if (a.sched && tid == 0) {
+    __threadfence();
+    const int nblk = (int)gridDim.x;
+    if (atomicAdd(a.sched, 1) == nblk - 1) {
+      atomicExch(a.sched + 1, 0);
+      atomicExch(a.sched, 0);
+    }
+  }
+}
+
+static int wino_num_cus() {
+  static int n = 0;
+  if (!n) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+  }
+  return n;
+}
+
+static int env_int(const char* n, int dflt) {
+  const char* v = getenv(n);
+  return (v && v[0]) ? atoi(v) : dflt;
+}
+
+template <int IOP, int POST, bool RES, int ACT>
+static int wino_launch4(const WinoArgs& a, int grid, hipStream_t s) {
+  const hipError_t e = hipFuncSetAttribute((const void*)conv_wino_kernel<IOP, POST, RES, ACT>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, kLds);
+  if (e != hipSuccess) return -(int)e;
+  hipLaunchKernelGGL((conv_wino_kernel<IOP, POST, RES, ACT>), dim3(grid), dim3(256), kLds, s, a);
+  FVC_CHECK_LAUNCH();
+  return 0;
+}
+
+// instantiated: Warp_net's forms (ResBlock conv1: ReLU in, ReLU act; conv2: residual, with or
+// without the pool), plus no-activation / LeakyReLU plain convs for the general entry point
+template <int IOP, int POST>
+static int wino_launch(const WinoArgs& a, int act, hipStream_t s, int grid) {
+  if (a.res) {
+    if (act == FVC_ACT_NONE) return wino_launch4<IOP, POST, true, FVC_ACT_NONE>(a, grid, s);
+    if (act == FVC_ACT_RELU) return wino_launch4<IOP, POST, true, FVC_ACT_RELU>(a, grid, s);
+    return wino_launch4<IOP, POST, true, FVC_ACT_LRELU>(a, grid, s);
+  }
+  if (act == FVC_ACT_NONE) return wino_launch4<IOP, POST, false, FVC_ACT_NONE>(a, grid, s);
+  if (act == FVC_ACT_RELU) return wino_launch4<IOP, POST, false, FVC_ACT_RELU>(a, grid, s);
+  return wino_launch4<IOP, POST, false, FVC_ACT_LRELU>(a, grid, s);
+}
+
+static int run_wino(const float* x, const void* upack, float osc, const float* bias, const float* res, float* y,
+                    float* pool, int batch, int h, int w, int in_op, int act, int cu_reserve, int* ovf, int* sched,
+                    int sched_len, hipStream_t s) {
+  if (!x || !upack || !bias || !y || batch <= 0 || h <= 0 || w <= 0 || cu_reserve < 0 || sched_len < 0)
+    return FVC_EINVAL;
+  if (in_op != FVC_IN_NONE && in_op != FVC_IN_RELU) return FVC_EINVAL;
+  const unsigned long long img = (unsigned long long)h * w * kC * 4ull;
+  const unsigned long long lim = (1ull << 32) - 4096;
+  if ((unsigned long long)batch * img >= lim) {
+    // y / res / pool through 32-bit buffer offsets: split the batch
+    if (batch == 1) return FVC_EINVAL;
+    const int b1 = batch / 2;
+    const size_t xs = (size_t)h * w * kC, ps = (size_t)(h / 2) * (w / 2) * kC;
+    int rc = run_wino(x, upack, osc, bias, res, y, pool, b1, h, w, in_op, act, cu_reserve, ovf, sched, sched_len, s);
+    if (rc) return rc;
+    return run_wino(x + b1 * xs, upack, osc, bias, res ? res + b1 * xs : nullptr, y + b1 * xs,
+                    pool ? pool + b1 * ps : nullptr, batch - b1, h, w, in_op, act, cu_reserve, ovf, sched, sched_len, s);
+  }
+  WinoArgs a;
+  a.x = x;
+  a.u = (const uint4*)upack;
+  a.bias = bias;
+  a.res = res;
+  a.y = y;
+  a.pool = pool;
+  a.B = batch;
+  a.H = h;
+  a.W = w;
+  a.tiles_y = (h + 1) / 2;
+  a.ngroups = fvc_cdiv(w, 32);
+  a.chunks_per_col = fvc_cdiv(a.tiles_y, kChunk);
+  a.nchunks = batch * a.ngroups * a.chunks_per_col;
+  a.osc = osc;
+  a.osc_c = osc * (1.0f / 2048.f);
+  a.y_bytes = (unsigned)(batch * img);
+  a.res_bytes = res ? (unsigned)(batch * img) : 0u;
+  a.pool_bytes = pool ? (unsigned)((unsigned long long)batch * (h / 2) * (w / 2) * kC * 4ull) : 0u;
+  a.x_bytes = (unsigned)(batch * img);
+  a.ovf = ovf;
+  const int reserve = env_int("FVC_X3_RESERVE", -1) >= 0 ? env_int("FVC_X3_RESERVE", 0) : cu_reserve;
+  const int ncu = wino_num_cus() - (reserve < wino_num_cus() / 2 ? reserve : wino_num_cus() / 2);
+  int grid = ncu < a.nchunks ? ncu : a.nchunks;
+  a.sched = (sched && sched_len >= 2 && env_int("FVC_X3_DYN", 1)) ? sched : nullptr;
+  if (act != FVC_ACT_NONE && act != FVC_ACT_RELU && act != FVC_ACT_LRELU) return FVC_EINVAL;
+  if (pool) {
+    if (in_op == FVC_IN_NONE) return wino_launch<FVC_IN_NONE, kPostPool>(a, act, s, grid);
+    return wino_launch<FVC_IN_RELU, kPostPool>(a, act, s, grid);
+  }
+  if (in_op == FVC_IN_NONE) return wino_launch<FVC_IN_NONE, 0>(a, act, s, grid);
+  return wino_launch<FVC_IN_RELU, 0>(a, act, s, grid);
+}
+
+static int x3w_kw(const double* u, size_t n) {
+  double mx = 0.0;
+  for (size_t i = 0; i < n; ++i) mx = fabs(u[i]) > mx ? fabs(u[i]) : mx;
+  if (!(mx > 0.0) || !isfinite(mx)) return 0;
+  int e;
+  frexp(mx, &e);
+  const int kw = 14 - e;  // mx * 2^kw in [2^13, 2^14)
+  return kw < -100 ? -100 : (kw > 100 ? 100 : kw);
+}
+
+}  // namespace
+
+extern "C" {
+
+int fvc_conv_wino_supported(int cin, int cout, int ksize, int stride, int transposed) {
+  return cin == kC && cout == kC && ksize == 3 && stride == 1 && !transposed;
+}
+
+size_t fvc_conv_wino_wpack_bytes(void) { return (size_t)16 * kC * kC * 2 * 2; }
+
+// w: [64][64][3][3] (OIHW, fp32). U[p = (r, q)][ci][co] = (G g G^T)[r][q] in double, scaled by 2^kw,
+// split into fp16 hi / lo*2^11 and laid out per wave r as [q][n][kk][plane][lane][8]: lane l holds
+// output channel 16n + (l & 15), input channels 32kk + 8(l >> 4) + 0..7 (the MFMA A operand).
+int fvc_conv_wino_pack_weight(const float* w, void* wp, float* osc_out) {
+  if (!w || !wp || !osc_out) return FVC_EINVAL;
+  static const double G[4][3] = {{1, 0, 0}, {0.5, 0.5, 0.5}, {0.5, -0.5, 0.5}, {0, 0, 1}};
+  double* U = (double*)malloc(sizeof(double) * 16 * kC * kC);  // [p][co][ci]
+  if (!U) return FVC_EINVAL;
+  for (int co = 0; co < kC; ++co)
+    for (int ci = 0; ci < kC; ++ci) {
+      const float* g = w + ((size_t)co * kC + ci) * 9;
+      double tmp[4][3];  // G g
+      for (int i = 0; i < 4; ++i)
+        for (int k = 0; k < 3; ++k) tmp[i][k] = G[i][0] * g[0 * 3 + k] + G[i][1] * g[1 * 3 + k] + G[i][2] * g[2 * 3 + k];
+      for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j)
+          U[((size_t)(i * 4 + j) * kC + co) * kC + ci] = tmp[i][0] * G[j][0] + tmp[i][1] * G[j][1] + tmp[i][2] * G[j][2];
+    }
+  const int kw = x3w_kw(U, (size_t)16 * kC * kC);
+  const double sc = ldexp(1.0, kw);
+  *osc_out = ldexpf(1.f, -kw);
+  _Float16* out = (_Float16*)wp;
+  for (int r = 0; r < 4; ++r)
+    for (int q = 0; q < 4; ++q)
+      for (int n = 0; n < 4; ++n)
+        for (int kk = 0; kk < 2; ++kk)
+          for (int lane = 0; lane < 64; ++lane) {
+            const int co = 16 * n + (lane & 15);
+            for (int e = 0; e < 8; ++e) {
+              const int ci = 32 * kk + 8 * (lane >> 4) + e;
+              const float v = (float)(U[((size_t)(r * 4 + q) * kC + co) * kC + ci] * sc);
+              const _Float16 hi = (_Float16)v;
+              const size_t base = ((((((size_t)r * 4 + q) * 4 + n) * 2 + kk) * 2) * 64 + lane) * 8;
+              out[base + e] = hi;                                               // plane 0
+              out[base + 64 * 8 + e] = (_Float16)((v - (float)hi) * 2048.f);   // plane 1
+            }
+          }
+  free(U);
+  return 0;
+}
+
+int fvc_conv2d_nhwc_wino(const float* x, const void* wpack, float osc, const float* bias, const float* res,
+                         float* y, float* pool, int batch, int h, int w, int in_op, int act, int cu_reserve,
+                         int* overflow_flag, int* sched, int sched_len, fvc_stream_t stream) {
+  return run_wino(x, wpack, osc, bias, res, y, pool, batch, h, w, in_op, act, cu_reserve, overflow_flag, sched,
+                  sched_len, (hipStream_t)stream);
+}
+
+}  // extern "C"

@@ -284,6 +284,16 @@ class PackedConv:
             self.bias = bias.detach().to(device, torch.float32).contiguous()
             return
         self.x3 = precision == "x3" and bool(lib.fvc_conv_x3_supported(cin, cout, ksize, stride, int(transposed)))
+        # 64 -> 64 3x3 stride-1 layers (Warp_net's ResBlocks): the Winograd F(2x2,3x3) split-precision
+        # kernel (fvc_conv_wino.hip; 2.25x fewer MFMAs); the direct x3 pack stays for the fused tap
+        # epilogue. FVC_WINO=0 disables it (A/B, tests).
+        self.wino = (self.x3 and os.environ.get("FVC_WINO", "1") != "0" and
+                     bool(lib.fvc_conv_wino_supported(cin, cout, ksize, stride, int(transposed))))
+        if self.wino:
+            upack = torch.empty(lib.fvc_conv_wino_wpack_bytes() // 2, dtype=torch.float16)
+            uosc = ctypes.c_float(0.0)
+            _lib.call("fvc_conv_wino_pack_weight", w.data_ptr(), upack.data_ptr(), ctypes.addressof(uosc))
+            self.upack, self.uosc = upack.to(device), float(uosc.value)
         if self.x3:
             nbytes = lib.fvc_conv_x3_wpack_bytes(cin, cout, ksize, stride, int(transposed))
             packed = torch.empty(nbytes // 2, dtype=torch.float16)
@@ -329,7 +339,13 @@ class PackedConv:
         if timer is not None:
             ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             ev0.record()
-        if self.x3:
+        wino = self.wino and in_op in (IN_NONE, IN_RELU) and post == POST_NONE
+        if wino:
+            _lib.call("fvc_conv2d_nhwc_wino", x.data_ptr(), self.upack.data_ptr(), self.uosc, self.bias.data_ptr(),
+                      _ptr(res), y.data_ptr(), None, B, H, W, in_op, act, _STATE["cu_reserve"],
+                      overflow_flag(x.device).data_ptr(), sched_scratch(x.device).data_ptr(), SCHED_LEN,
+                      stream_handle())
+        elif self.x3:
             fn = "fvc_deconv2d_nhwc_x3" if self.transposed else "fvc_conv2d_nhwc_x3"
             _lib.call(fn, x.data_ptr(), self.wpack.data_ptr(), self.osc, self.bias.data_ptr(), _ptr(res),
                       y.data_ptr(), B, H, W, self.cin, self.cout, self.ksize, self.stride, in_op, act, post,
@@ -347,14 +363,14 @@ class PackedConv:
             timer.records.append((ev0, ev1, profiling.conv_flops(self.cin, self.cout, self.ksize, self.stride,
                                                                  self.transposed, B, H, W),
                                   f"{'deconv' if self.transposed else 'conv'}{self.ksize}s{self.stride} "
-                                  f"{self.cin}->{self.cout} @{H}x{W}{' x3' if self.x3 else ''}", self.x3,
-                                  nbytes))
+                                  f"{self.cin}->{self.cout} @{H}x{W}{' wino' if wino else (' x3' if self.x3 else '')}",
+                                  self.x3, nbytes, "wino" if wino else ("x3" if self.x3 else "f32")))
         return y
 
 
     def pool_fusable(self) -> bool:
         return (self.x3 and self.tap is None and not self.transposed and self.stride == 1 and
-                bool(_lib.load().fvc_conv_x3_pool_supported(self.cin, self.cout, self.ksize)))
+                (self.wino or bool(_lib.load().fvc_conv_x3_pool_supported(self.cin, self.cout, self.ksize))))
 
     def call_pool(self, x, act=ACT_NONE, res=None):
         """(y, avg_pool2d(y, 2)) from one launch (fvc_conv2d_nhwc_x3_pool; in_op none, post none)."""
@@ -372,16 +388,23 @@ class PackedConv:
         if timer is not None:
             ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             ev0.record()
-        _lib.call("fvc_conv2d_nhwc_x3_pool", x.data_ptr(), self.wpack.data_ptr(), self.osc, self.bias.data_ptr(),
-                  _ptr(res), y.data_ptr(), pool.data_ptr(), B, H, W, self.cin, self.cout, self.ksize, act,
-                  _STATE["cu_reserve"], overflow_flag(x.device).data_ptr(), sched_scratch(x.device).data_ptr(),
-                  SCHED_LEN, stream_handle())
+        if self.wino:
+            _lib.call("fvc_conv2d_nhwc_wino", x.data_ptr(), self.upack.data_ptr(), self.uosc, self.bias.data_ptr(),
+                      _ptr(res), y.data_ptr(), pool.data_ptr(), B, H, W, IN_NONE, act, _STATE["cu_reserve"],
+                      overflow_flag(x.device).data_ptr(), sched_scratch(x.device).data_ptr(), SCHED_LEN,
+                      stream_handle())
+        else:
+            _lib.call("fvc_conv2d_nhwc_x3_pool", x.data_ptr(), self.wpack.data_ptr(), self.osc, self.bias.data_ptr(),
+                      _ptr(res), y.data_ptr(), pool.data_ptr(), B, H, W, self.cin, self.cout, self.ksize, act,
+                      _STATE["cu_reserve"], overflow_flag(x.device).data_ptr(), sched_scratch(x.device).data_ptr(),
+                      SCHED_LEN, stream_handle())
         if timer is not None:
             ev1.record()
             nbytes = 4 * (x.numel() + y.numel() * (2 if res is not None else 1) + pool.numel()) + \
                 self.wpack.numel() * self.wpack.element_size()
             timer.records.append((ev0, ev1, profiling.conv_flops(self.cin, self.cout, self.ksize, 1, False, B, H, W),
-                                  f"conv{self.ksize}s1 {self.cin}->{self.cout} @{H}x{W} x3 +pool", True, nbytes))
+                                  f"conv{self.ksize}s1 {self.cin}->{self.cout} @{H}x{W} {'wino' if self.wino else 'x3'} +pool",
+                                  True, nbytes, "wino" if self.wino else "x3"))
         return y, pool
 
     def tap_fusable(self, tap: "TapConsumer") -> bool:
@@ -424,7 +447,7 @@ class PackedConv:
                 self.wpack.numel() * self.wpack.element_size() + tap.wpack.numel() * tap.wpack.element_size()
             timer.records.append((ev0, ev1, fl, f"{'deconv' if self.transposed else 'conv'}{self.ksize}s{self.stride} "
                                   f"{self.cin}->{self.cout} @{H}x{W} x3 +tap{tap.ksize}x{tap.ksize}->{tap.cout}",
-                                  True, nbytes))
+                                  True, nbytes, "x3"))
         return P
 
 

@@ -34,19 +34,24 @@ class KernelTimer:
         global _ACTIVE
         _ACTIVE = None
 
-    def collect(self, x3=None):
+    def _select(self, x3, family):
+        return [r for r in self.records if (x3 is None or (len(r) > 4 and r[4]) == x3) and
+                (family is None or (len(r) > 6 and r[6] == family))]
+
+    def collect(self, x3=None, family=None):
         """Synchronise and return (total_ms, total_flops, n_launches); x3=True/False restricts to
-        the split-precision / the fp32+VALU conv launches."""
+        the split-precision / the fp32+VALU conv launches, family to one kernel ('x3': the direct
+        conv_x3_kernel, 'wino': conv_wino_kernel, 'f32')."""
         torch.cuda.synchronize()
-        rs = [r for r in self.records if x3 is None or (len(r) > 4 and r[4]) == x3]
+        rs = self._select(x3, family)
         ms = sum(r[0].elapsed_time(r[1]) for r in rs)
         fl = sum(r[2] for r in rs)
         return ms, fl, len(rs)
 
-    def collect_bytes(self, x3=None):
+    def collect_bytes(self, x3=None, family=None):
         """Algorithmic HBM bytes (input + packed weights + output + residual) of the launches
-        ``collect(x3)`` counts."""
-        return sum(r[5] for r in self.records if len(r) > 5 and (x3 is None or r[4] == x3))
+        ``collect(x3, family)`` counts."""
+        return sum(r[5] for r in self._select(x3, family) if len(r) > 5)
 
     def collect_hbm(self):
         """{name: [launches, ms, algorithmic bytes]} of the HBM-bound (non-conv) kernels."""

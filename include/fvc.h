@@ -133,6 +133,19 @@ int fvc_deconv2d_nhwc_x3_tap(const float* x, const void* wpack, float osc, const
                              int ksize, int stride, int act, const void* tap_wpack, float tap_osc,
                              int pcp, int cu_reserve, int* overflow_flag, int* sched, int sched_len,
                              fvc_stream_t stream);
+/* Winograd F(2x2,3x3) split-precision conv for the 64 -> 64-channel 3x3 stride-1 pad-1 layers
+ * (Warp_net ResBlocks, endecoder.py:228-296; same contract as fvc_conv2d_nhwc_x3 with cin = cout =
+ * 64, in_op none / relu, act, res; pool != NULL additionally writes avg_pool2d(y, 2) as
+ * fvc_conv2d_nhwc_x3_pool: [batch][h/2][w/2][64], floor sizes). The transformed weights U = G g G^T (computed in double,
+ * split fp16 hi/lo) come from fvc_conv_wino_pack_weight (host, fvc_conv_wino_wpack_bytes() bytes,
+ * w OIHW [64][64][3][3]). sched: >= 2 ints, zero between launches (shared with the x3 kernels). */
+int fvc_conv_wino_supported(int cin, int cout, int ksize, int stride, int transposed);
+size_t fvc_conv_wino_wpack_bytes(void);
+int fvc_conv_wino_pack_weight(const float* w_host, void* wpack_host, float* osc_out);
+int fvc_conv2d_nhwc_wino(const float* x, const void* wpack, float osc, const float* bias,
+                         const float* res, float* y, float* pool, int batch, int h, int w, int in_op,
+                         int act, int cu_reserve, int* overflow_flag, int* sched, int sched_len,
+                         fvc_stream_t stream);
 
 /* ------------------------------------------------------------------ layout / resampling */
 int fvc_nchw_to_nhwc(const float* src, float* dst, int batch, int c, int h, int w, int cp,

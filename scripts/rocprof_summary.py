@@ -1,6 +1,7 @@
 """Summarise a rocprofv3 --kernel-trace --stats run of `bench.py --serial` per P-frame and
 (optionally) the FETCH_SIZE/WRITE_SIZE PMC passes over the same command, for comparison with
-bench.py's roofline object (which times conv_x3_kernel with HIP events on its stream).
+bench.py's roofline object (which times the split-precision conv kernels -- conv_x3_kernel and
+conv_wino_kernel -- with HIP events on their stream).
 
 usage: python scripts/rocprof_summary.py <stats_csv> <n_pframes_total>
            [--fetch fetch_counter_collection.csv --write write_counter_collection.csv
@@ -10,9 +11,11 @@ import argparse
 import csv
 import json
 
-CONV_PREFIXES = ("conv_x3_kernel", "conv_mfma_f32_kernel", "conv_mfma_pipe_kernel", "deconv2_mfma_f32_kernel",
-                 "conv_smalln_f32_kernel")
+CONV_PREFIXES = ("conv_x3_kernel", "conv_wino_kernel", "conv_mfma_f32_kernel", "conv_mfma_pipe_kernel",
+                 "deconv2_mfma_f32_kernel", "conv_smalln_f32_kernel")
 X3 = "conv_x3_kernel"
+WINO = "conv_wino_kernel"
+SPLIT = (X3, WINO)  # the split-precision conv family bench.py's roofline object covers
 
 
 def is_conv(name):
@@ -44,13 +47,18 @@ def main():
     tot = sum(float(r["TotalDurationNs"]) for r in rows)
     conv = sum(float(r["TotalDurationNs"]) for r in rows if is_conv(r["Name"]))
     calls = sum(int(r["Calls"]) for r in rows if is_conv(r["Name"]))
-    x3_ns = sum(float(r["TotalDurationNs"]) for r in rows if X3 in r["Name"])
-    x3_calls = sum(int(r["Calls"]) for r in rows if X3 in r["Name"])
     print(f"all kernels: {tot / 1e6:.2f} ms total, {tot / 1e6 / nframes:.3f} ms per P-frame")
     print(f"conv family: {conv / 1e6:.2f} ms total over {calls} launches, {conv / 1e6 / nframes:.3f} ms per P-frame")
-    if x3_calls:
-        print(f"{X3} (all instantiations): {x3_calls} launches, avg {x3_ns / x3_calls / 1e3:.2f} us, "
-              f"{x3_ns / 1e6 / nframes:.3f} ms per P-frame")
+    per = {}
+    for k in SPLIT + ("split",):
+        keys = SPLIT if k == "split" else (k,)
+        ns = sum(float(r["TotalDurationNs"]) for r in rows if any(x in r["Name"] for x in keys))
+        n = sum(int(r["Calls"]) for r in rows if any(x in r["Name"] for x in keys))
+        per[k] = (ns, n)
+        if n:
+            label = "split-precision family (" + " + ".join(SPLIT) + ")" if k == "split" else f"{k} (all instantiations)"
+            print(f"{label}: {n} launches, avg {ns / n / 1e3:.2f} us, {ns / 1e6 / nframes:.3f} ms per P-frame")
+    x3_ns, x3_calls = per["split"]
     print("top kernels (ms per P-frame):")
     for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"]))[:15]:
         print(f"  {float(r['TotalDurationNs']) / 1e6 / nframes:8.3f}  n/frame={int(r['Calls']) / nframes:6.1f}  "
@@ -58,21 +66,35 @@ def main():
     if a.fetch and a.write:
         # gfx950: FETCH_SIZE tallies 128-B requests at 64 B -> x2 (MI355X_MICROARCH.md, HBM section);
         # WRITE_SIZE exact for 16-B-per-lane stores (the x3 epilogue stores float4)
-        f = pmc_per_dispatch(a.fetch, "FETCH_SIZE", X3)
-        w = pmc_per_dispatch(a.write, "WRITE_SIZE", X3)
-        fb = 2.0 * sum(f.values()) / max(1, len(f))
-        wb = sum(w.values()) / max(1, len(w))
+        out = {"height": a.height, "width": a.width,
+               "correction": "FETCH_SIZE x2 (gfx950 wide-read tally), WRITE_SIZE x1"}
+        fam_f, fam_w = {}, {}
+        for k in SPLIT:
+            f = pmc_per_dispatch(a.fetch, "FETCH_SIZE", k)
+            w = pmc_per_dispatch(a.write, "WRITE_SIZE", k)
+            fam_f.update(f)
+            fam_w.update(w)
+            if not f:
+                continue
+            fb = 2.0 * sum(f.values()) / len(f)
+            wb = sum(w.values()) / max(1, len(w))
+            print(f"{k}: {len(f)} dispatches with FETCH_SIZE, {len(w)} with WRITE_SIZE; per launch "
+                  f"fetch {fb / 1e6:.3f} MB (x2 corrected), write {wb / 1e6:.3f} MB")
+            ns, n = per[k]
+            out[k] = {"launches": len(f), "fetch_bytes_per_launch": round(fb), "write_bytes_per_launch": round(wb),
+                      "hbm_bytes_per_launch": round(fb + wb),
+                      "avg_launch_us_kernel_trace": round(ns / n / 1e3, 2) if n else None}
+        fb = 2.0 * sum(fam_f.values()) / max(1, len(fam_f))
+        wb = sum(fam_w.values()) / max(1, len(fam_w))
         fc = 2.0 * sum(v for k, v in pmc_per_dispatch(a.fetch, "FETCH_SIZE", "").items()) / 1e9
-        print(f"{X3}: {len(f)} dispatches with FETCH_SIZE, {len(w)} with WRITE_SIZE; per launch "
-              f"fetch {fb / 1e6:.3f} MB (x2 corrected), write {wb / 1e6:.3f} MB")
         print(f"all kernels FETCH (x2): {fc:.3f} GB")
+        # top-level fields: the split-precision family (bench.py's roofline object)
+        out.update({"kernel": " + ".join(SPLIT), "launches": len(fam_f), "fetch_bytes_per_launch": round(fb),
+                    "write_bytes_per_launch": round(wb), "hbm_bytes_per_launch": round(fb + wb),
+                    "avg_launch_us_kernel_trace": round(x3_ns / x3_calls / 1e3, 2) if x3_calls else None})
         if a.json_out:
             with open(a.json_out, "w") as fo:
-                json.dump({"kernel": X3, "height": a.height, "width": a.width, "launches": len(f),
-                           "fetch_bytes_per_launch": round(fb), "write_bytes_per_launch": round(wb),
-                           "hbm_bytes_per_launch": round(fb + wb),
-                           "avg_launch_us_kernel_trace": round(x3_ns / x3_calls / 1e3, 2) if x3_calls else None,
-                           "correction": "FETCH_SIZE x2 (gfx950 wide-read tally), WRITE_SIZE x1"}, fo, indent=1)
+                json.dump(out, fo, indent=1)
             print("wrote", a.json_out)
 
 

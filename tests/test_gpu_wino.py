@@ -1,0 +1,157 @@
+"""The Winograd F(2x2,3x3) split-precision conv (fvc_conv_wino.hip) against float64 torch convs of
+the same op (the ATen conv2d the reference's Warp_net ResBlocks call, endecoder.py:228-296) and
+against the direct split-precision kernel: ragged sizes (tile rows, 32-column groups and images
+cut at the edges), every epilogue form (ReLU input, ReLU / none activation, residual, the fused
+2x2 pool), the dynamic and static schedules, the 32-bit-offset batch split, determinism and the
+overflow flag."""
+import os
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from fastvideocodec_amd import kernels as K
+
+pytestmark = pytest.mark.gpu
+
+
+def to_nhwc(x):
+    return x.permute(0, 2, 3, 1).contiguous()
+
+
+def from_nhwc(y):
+    return y.permute(0, 3, 1, 2).contiguous()
+
+
+def _packs(dev, w, b):
+    """(winograd, direct x3) packs of the same 64->64 3x3 layer."""
+    pw = K.PackedConv(w, b, 3, 1, False, dev, precision="x3")
+    assert pw.wino
+    old = os.environ.get("FVC_WINO")
+    os.environ["FVC_WINO"] = "0"
+    try:
+        pd = K.PackedConv(w, b, 3, 1, False, dev, precision="x3")
+    finally:
+        if old is None:
+            del os.environ["FVC_WINO"]
+        else:
+            os.environ["FVC_WINO"] = old
+    assert not pd.wino and pd.x3
+    return pw, pd
+
+
+def _ref(x, w, b, in_relu, act_relu, res):
+    xr = torch.relu(x) if in_relu else x
+    y = F.conv2d(xr.double(), w.double(), b.double(), 1, 1)
+    if act_relu:
+        y = torch.relu(y)
+    if res is not None:
+        y = y + res.double()
+    return y
+
+
+# (B, H, W, in_relu, act_relu, with_res): Warp_net's forms, sizes cut at every edge
+CASES = [
+    (1, 40, 72, True, True, False),    # ResBlock conv1
+    (2, 37, 70, False, False, True),   # ResBlock conv2 (residual), odd height, partial column group
+    (1, 2, 30, True, False, False),    # a single tile row narrower than one column group
+    (3, 68, 120, True, True, True),
+    (1, 136, 96, False, True, False),  # more than one 16-row schedule chunk per column
+]
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_wino_vs_float64_and_direct(dev, case):
+    B, H, W, in_relu, act_relu, with_res = case
+    g = torch.Generator().manual_seed(100 + H)
+    x = torch.randn(B, 64, H, W, generator=g)
+    w = torch.randn(64, 64, 3, 3, generator=g) * 0.05
+    b = torch.randn(64, generator=g) * 0.1
+    res = torch.randn(B, 64, H, W, generator=g) if with_res else None
+    ref = _ref(x, w, b, in_relu, act_relu, res)
+    pw, pd = _packs(dev, w, b)
+    kw = dict(in_op=K.IN_RELU if in_relu else K.IN_NONE, act=K.ACT_RELU if act_relu else K.ACT_NONE,
+              res=to_nhwc(res).to(dev) if with_res else None)
+    xd = to_nhwc(x).to(dev)
+    yw, yd = pw(xd, **kw), pd(xd, **kw)
+    torch.cuda.synchronize()
+    ew = float((from_nhwc(yw.cpu()).double() - ref).abs().max())
+    ed = float((from_nhwc(yd.cpu()).double() - ref).abs().max())
+    scale = float(ref.abs().max())
+    print(f"{case}: wino err {ew / scale:.2e}, direct x3 err {ed / scale:.2e} (of output scale)")
+    # split-precision accuracy (test_gpu_kernels: direct x3 3-4e-7, fp32-MFMA ~1e-6 of scale)
+    assert ew <= 2e-6 * scale, (ew, ed, scale)
+
+
+@pytest.mark.parametrize("xscale", [1e-4, 1.0, 3000.0])
+def test_wino_accuracy_across_activation_scales(dev, xscale):
+    """Winograd's transforms add and subtract up to 4 inputs (and 4 products per output): the
+    error stays at the split-precision level from tiny to large activations, and within 2x the
+    fp32-MFMA kernel's own error."""
+    g = torch.Generator().manual_seed(12)
+    x = (torch.rand(1, 64, 40, 72, generator=g) - 0.3) * xscale
+    w = torch.randn(64, 64, 3, 3, generator=g) * 0.04
+    b = torch.randn(64, generator=g) * 0.1 * xscale
+    ref = F.conv2d(x.double(), w.double(), b.double(), 1, 1)
+    xd = to_nhwc(x).to(dev)
+    pw = K.PackedConv(w, b, 3, 1, False, dev, precision="x3")
+    assert pw.wino
+    yw = pw(xd)
+    y32 = K.PackedConv(w, b, 3, 1, False, dev, precision="f32")(xd)
+    torch.cuda.synchronize()
+    ew = float((from_nhwc(yw.cpu()).double() - ref).abs().max())
+    e32 = float((from_nhwc(y32.cpu()).double() - ref).abs().max())
+    scale = float(ref.abs().max())
+    print(f"xscale {xscale}: wino err {ew / scale:.2e}, f32 err {e32 / scale:.2e}")
+    assert ew <= 4e-6 * scale and ew <= 2 * e32 + 1e-7 * scale, (ew, e32, scale)
+
+
+def test_wino_pool_epilogue_bitexact(dev):
+    """call_pool on the Winograd kernel: y equals the plain launch bit for bit and pool equals
+    fvc_avgpool2_nhwc of y bit for bit (ATen's summation order)."""
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(2, 64, 36, 98, generator=g)
+    w = torch.randn(64, 64, 3, 3, generator=g) * 0.05
+    b = torch.randn(64, generator=g) * 0.1
+    res = to_nhwc(torch.randn(2, 64, 36, 98, generator=g)).to(dev)
+    pw, _ = _packs(dev, w, b)
+    xd = to_nhwc(x).to(dev)
+    y, p = pw.call_pool(xd, res=res)
+    y2 = pw(xd, res=res)
+    p2 = K.avgpool2(y)
+    torch.cuda.synchronize()
+    assert torch.equal(y, y2)
+    assert torch.equal(p, p2)
+
+
+def test_wino_schedules_and_determinism(dev, monkeypatch):
+    """Dynamic (counter) and static chunk schedules and repeated launches give identical bits; the
+    schedule scratch is left zeroed."""
+    g = torch.Generator().manual_seed(6)
+    x = to_nhwc(torch.randn(2, 64, 100, 130, generator=g)).to(dev)
+    w = torch.randn(64, 64, 3, 3, generator=g) * 0.05
+    pw, _ = _packs(dev, w, torch.zeros(64))
+    a = pw(x, in_op=K.IN_RELU, act=K.ACT_RELU)
+    b = pw(x, in_op=K.IN_RELU, act=K.ACT_RELU)
+    monkeypatch.setenv("FVC_X3_DYN", "0")
+    c = pw(x, in_op=K.IN_RELU, act=K.ACT_RELU)
+    monkeypatch.setenv("FVC_X3_RESERVE", "100")
+    d = pw(x, in_op=K.IN_RELU, act=K.ACT_RELU)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b) and torch.equal(a, c) and torch.equal(a, d)
+    assert int(K.sched_scratch(dev)[:2].abs().sum()) == 0
+
+
+def test_wino_overflow_flag(dev):
+    """A transformed input >= 65000 cannot be split into fp16 halves: the kernel raises the
+    stream's overflow flag (here one input of 7e4)."""
+    g = torch.Generator().manual_seed(7)
+    w = torch.randn(64, 64, 3, 3, generator=g) * 0.05
+    pw, _ = _packs(dev, w, torch.zeros(64))
+    x = torch.randn(1, 64, 16, 32, generator=g)
+    K.x3_overflow(reset=True)
+    pw(to_nhwc(x).to(dev))
+    assert not K.x3_overflow(reset=True)
+    x[0, 5, 7, 9] = 7e4
+    pw(to_nhwc(x).to(dev))
+    assert K.x3_overflow(reset=True)
