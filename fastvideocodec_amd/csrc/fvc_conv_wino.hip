@@ -14,8 +14,11 @@
 //
 // Numerics as fvc_conv_x3.hip: U (scaled by 2^kw so max|U| is in [2^13, 2^14)) and V (fp32 here)
 // are split exactly into fp16 hi + lo * 2^-11; main += U_hi V_hi and corr += U_lo V_hi + U_hi V_lo
-// in two fp32 accumulators. |V| <= 4 max|x|: a transformed value >= 65000 (or NaN) sets the
-// caller's overflow flag (the host then recomputes on the fp32 kernels).
+// in two fp32 accumulators. |V| <= 4 max|x|: a transformed value >= 65520 rounds to an infinite hi
+// part, whose products reach every output of its tile that lies in the image as inf / NaN (the
+// B^T / A^T patterns leave no overflowing position feeding only clipped outputs); the kernel sums
+// 0 * output and raises the caller's overflow flag on a NaN (the host then recomputes on the fp32
+// kernels). NaN inputs raise it as well.
 //
 // Resident weights: one 256-thread block per CU, one wave per SIMD with 512 registers. Wave r owns
 // row r of the 4x4 transform domain (positions (r, q), q = 0..3) for all 64 output channels: its
@@ -25,8 +28,8 @@
 // operand of its wave's 4 positions (no V in memory). The waves then exchange the column-combined
 // partial results Z[r][j] = sum_q M[r][q] A[q][j] through LDS (double-buffered: one barrier per
 // item) and wave w finishes output channels 16w .. 16w+15: Y[i][j] = sum_r A^T[i][r] Z[r][j].
-// Input: a ring of 8 raw fp32 input rows in LDS filled by LDS-DMA (global_load_lds_dwordx4, a zero
-// page for the padding); consecutive items of a block walk down one tile column, so each item
+// Input: a ring of 8 raw fp32 input rows in LDS filled by LDS-DMA (buffer_load_dwordx4 ... lds, one
+// descriptor per row: padding rows and columns read past it and land as zeros); consecutive items of a block walk down one tile column, so each item
 // stages the 2 new rows of its 4-row window while the previous item computes.
 // LDS input layout: row slot -> 16 channel quads -> 40 column slots of 16 B, even columns 0..16 then
 // odd columns 17..33 (the tile columns of a patch are 2 apart): a lane group's ds_read_b128 of 16
@@ -59,11 +62,14 @@ constexpr int kHdr = 512;                             // bias (256 B) + schedule
 constexpr int kLds = kHdr + kRingBytes + 2 * kZBytes; // 148,480 B
 constexpr int kChunk = 16;         // items per schedule chunk (consecutive tile rows of one column)
 constexpr float kLoScale = 2048.f;
+#ifndef FVC_WINO_ALLNOP
+#define FVC_WINO_ALLNOP 0
+#endif
+constexpr bool kAllNop = FVC_WINO_ALLNOP;  // every MFMA block opens with s_nop 1 (diagnostic)
 constexpr unsigned kOob = 0xFFFFFF00u;
 constexpr int kRsrcFlags = 0x00020000;
 constexpr int kPostPool = 1;
 
-__device__ __attribute__((aligned(16))) float g_wino_zero[4];  // zero page for padding pixels
 
 struct WinoArgs {
   const float* x;
@@ -76,43 +82,15 @@ struct WinoArgs {
   int tiles_y, ngroups;  // tile rows, 32-column groups
   int nchunks, chunks_per_col;
   float osc, osc_c;      // 2^-kw, 2^-kw-11
-  unsigned y_bytes, res_bytes, pool_bytes, x_bytes;
   int* sched;            // [0] blocks finished, [1] next chunk; zero on entry, reset by the last block
   int* ovf;
 };
 
-__device__ __forceinline__ unsigned lds_addr(const void* p) {
-  return __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)((const __attribute__((address_space(3))) char*)p));
-}
+typedef __attribute__((address_space(3))) void* lds_ptr;
 
-// One 1-KB LDS-DMA piece: lane l's 16 B at g land at LDS byte lds + 16 l (M0 saved and restored;
-// the kernel drains these itself with vmcnt(0) before the barrier that publishes the rows).
-__device__ __forceinline__ void glds16(const void* g, unsigned lds) {
-  unsigned keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep)
-               : "v"(g), "s"(lds)
-               : "memory");
-}
-
-// v = hi + lo * 2^-11 for 8 values; mx tracks max |v|. Scalar f32 arithmetic: packed f32 VALU
-// (v_pk_*_f32) issues slower than two plain ops beside MFMAs (MI355X_MICROARCH.md, fillers).
-__device__ __forceinline__ void split8(const float (&v)[8], h8& hi, h8& lo, float& mx) {
-#pragma unroll
-  for (int i = 0; i < 8; i += 2) {
-    const f2v x = {v[i], v[i + 1]};
-    const h2v h = __builtin_convertvector(x, h2v);  // v_cvt_pk_f16_f32 (round to nearest even)
-    const float d0 = (v[i] - (float)h[0]) * kLoScale;
-    const float d1 = (v[i + 1] - (float)h[1]) * kLoScale;
-    const f2v d = {d0, d1};
-    const h2v l = __builtin_convertvector(d, h2v);
-    hi[i] = h[0];
-    hi[i + 1] = h[1];
-    lo[i] = l[0];
-    lo[i + 1] = l[1];
-  }
-  mx = fmaxf(mx, fmaxf(fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))),
-                       fmaxf(fmaxf(fabsf(v[4]), fabsf(v[5])), fmaxf(fabsf(v[6]), fabsf(v[7])))));
+// a raw buffer descriptor over [p, p + bytes): offsets at or past `bytes` read 0 / drop the store
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, (int)bytes, kRsrcFlags);
 }
 
 // The three split-precision products of one (position, 16-channel N-tile) pair:
@@ -123,26 +101,53 @@ __device__ __forceinline__ void split8(const float (&v)[8], h8& hi, h8& lo, floa
 // or a v_accvgpr_write of U right before -> 2 states (s_nop 1, opening the string); the
 // accumulate chains need none; the VALU reads of acc / cor after the item's last MFMA are fenced
 // by wino_mfma_drain.
-template <bool FIRST>
+// NOP: open with the 2 states (s_nop 1) a VALU-written vh / vl needs; blocks whose operands were
+// written three or more instructions earlier skip it (scripts/check_wino_hazards.py audits the
+// built .s for VALU writes of MFMA sources within 2 states).
+#define WINO_MFMA3_BODY(C0, C1)                    \
+  "v_mfma_f32_16x16x32_f16 %0, %2, %4, " C0 "\n\t" \
+  "v_mfma_f32_16x16x32_f16 %1, %3, %4, " C1 "\n\t" \
+  "v_mfma_f32_16x16x32_f16 %1, %2, %5, %1"
+template <bool FIRST, bool NOP>
 __device__ __forceinline__ void wino_mfma3(f32x4& acc, f32x4& cor, const h8& uh, const h8& ul, const h8& vh,
                                            const h8& vl) {
   if constexpr (FIRST) {  // first k-step of an item: the chains start from C = 0
-    asm volatile(
-        "s_nop 1\n\t"
-        "v_mfma_f32_16x16x32_f16 %0, %2, %4, 0\n\t"
-        "v_mfma_f32_16x16x32_f16 %1, %3, %4, 0\n\t"
-        "v_mfma_f32_16x16x32_f16 %1, %2, %5, %1"
-        : "=&v"(acc), "=&v"(cor)
-        : "a"(uh), "a"(ul), "v"(vh), "v"(vl));
+    if constexpr (NOP)
+      asm volatile("s_nop 1\n\t" WINO_MFMA3_BODY("0", "0") : "=&v"(acc), "=&v"(cor) : "a"(uh), "a"(ul), "v"(vh), "v"(vl));
+    else
+      asm volatile(WINO_MFMA3_BODY("0", "0") : "=&v"(acc), "=&v"(cor) : "a"(uh), "a"(ul), "v"(vh), "v"(vl));
   } else {
-    asm volatile(
-        "s_nop 1\n\t"
-        "v_mfma_f32_16x16x32_f16 %0, %2, %4, %0\n\t"
-        "v_mfma_f32_16x16x32_f16 %1, %3, %4, %1\n\t"
-        "v_mfma_f32_16x16x32_f16 %1, %2, %5, %1"
-        : "+v"(acc), "+v"(cor)
-        : "a"(uh), "a"(ul), "v"(vh), "v"(vl));
+    if constexpr (NOP)
+      asm volatile("s_nop 1\n\t" WINO_MFMA3_BODY("%0", "%1") : "+v"(acc), "+v"(cor) : "a"(uh), "a"(ul), "v"(vh), "v"(vl));
+    else
+      asm volatile(WINO_MFMA3_BODY("%0", "%1") : "+v"(acc), "+v"(cor) : "a"(uh), "a"(ul), "v"(vh), "v"(vl));
   }
+}
+
+// wino_mfma3 (first k-step) followed by the split of two values of the next k-step (split2's
+// instructions): the split's VALU issues while this block's MFMAs run instead of in a cluster of
+// its own. Its outputs feed MFMAs of the next k-step, blocks later.
+#define WINO_MFMA3S_BODY                                                     \
+  "v_mfma_f32_16x16x32_f16 %0, %7, %9, 0\n\t"                              \
+  "v_cvt_pk_f16_f32 %2, %11, %12\n\t"                                      \
+  "v_mfma_f32_16x16x32_f16 %1, %8, %9, 0\n\t"                              \
+  "v_fma_mix_f32 %4, %2, -1.0, %11 op_sel_hi:[1,0,0]\n\t"                  \
+  "v_fma_mix_f32 %5, %2, -1.0, %12 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\t"   \
+  "v_mfma_f32_16x16x32_f16 %1, %7, %10, %1\n\t"                            \
+  "v_fma_mixlo_f16 %3, %4, %6, 0\n\t"                                      \
+  "v_fma_mixhi_f16 %3, %5, %6, 0"
+template <bool NOP>
+__device__ __forceinline__ void wino_mfma3_split(f32x4& acc, f32x4& cor, const h8& uh, const h8& ul, const h8& vh,
+                                                 const h8& vl, float v0, float v1, unsigned& hi, unsigned& lo) {
+  float r0, r1;
+  if constexpr (NOP)
+    asm volatile("s_nop 1\n\t" WINO_MFMA3S_BODY
+                 : "=&v"(acc), "=&v"(cor), "=&v"(hi), "=&v"(lo), "=&v"(r0), "=&v"(r1)
+                 : "s"(kLoScale), "a"(uh), "a"(ul), "v"(vh), "v"(vl), "v"(v0), "v"(v1));
+  else
+    asm volatile(WINO_MFMA3S_BODY
+                 : "=&v"(acc), "=&v"(cor), "=&v"(hi), "=&v"(lo), "=&v"(r0), "=&v"(r1)
+                 : "s"(kLoScale), "a"(uh), "a"(ul), "v"(vh), "v"(vl), "v"(v0), "v"(v1));
 }
 
 // 12 wait states after the last MFMA of an item (the 8-pass XDL bound, cdna_hip_programming.md
@@ -172,14 +177,12 @@ __device__ __forceinline__ float relu1(float x) {
 // convert). Pure VALU asm: the hardware interlocks VALU dependencies.
 __device__ __forceinline__ void split2(float v0, float v1, unsigned& hi, unsigned& lo) {
   float r0, r1;
-  asm volatile(
-      "v_cvt_pk_f16_f32 %0, %3, %4\n\t"
+  asm("v_cvt_pk_f16_f32 %0, %3, %4\n\t"
       "v_fma_mix_f32 %1, %0, -1.0, %3 op_sel_hi:[1,0,0]\n\t"
       "v_fma_mix_f32 %2, %0, -1.0, %4 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
       : "=&v"(hi), "=&v"(r0), "=&v"(r1)
       : "v"(v0), "v"(v1));
-  asm volatile(
-      "v_fma_mixlo_f16 %0, %1, %3, 0\n\t"
+  asm("v_fma_mixlo_f16 %0, %1, %3, 0\n\t"
       "v_fma_mixhi_f16 %0, %2, %3, 0"
       : "=&v"(lo)
       : "v"(r0), "v"(r1), "s"(kLoScale));
@@ -223,7 +226,7 @@ __global__ __launch_bounds__(256, 1) void conv_wino_kernel(const WinoArgs a) {
   const float sb = wave == 1 ? 1.f : -1.f;
 
   // DMA pieces of a staged row this wave issues (piece k of 10 -> wave k & 3) and the lane's
-  // part of each: local input column (or -1: pad slot) and channel-quad offset
+  // part of each: local input column (or a pad slot) and channel-quad offset
   int dma_lc[3], dma_ch[3];
 #pragma unroll
   for (int m = 0; m < 3; ++m) {
@@ -233,17 +236,26 @@ __global__ __launch_bounds__(256, 1) void conv_wino_kernel(const WinoArgs a) {
     dma_ch[m] = 4 * c4;
   }
   const int npiece = wave < 2 ? 3 : 2;  // 10 pieces over 4 waves
-  // stage input row iy of image b, column group g into ring slot s
-  auto stage_row = [&](int b, int g, int iy, int s) {
+  // byte offsets of the lane's pieces within an input row of column group g (past the row for
+  // padding columns and pad slots: the buffer unit returns zeros)
+  auto row_offsets = [&](int g, unsigned (&vo)[3]) {
+#pragma unroll
+    for (int m = 0; m < 3; ++m) {
+      const int ix = 32 * g - 1 + dma_lc[m];
+      vo[m] = (unsigned)ix < (unsigned)W ? (unsigned)(ix * kC + dma_ch[m]) * 4u : kOob;
+    }
+  };
+  const unsigned row_bytes = (unsigned)W * kC * 4u;
+  // stage input row iy of image b into ring slot s: one descriptor per row (0 bytes for a
+  // padding row), the lane offsets of its column group
+  auto stage_row = [&](int b, int iy, int s, const unsigned (&vo)[3]) {
     const bool row_ok = (unsigned)iy < (unsigned)H;
-    const size_t rowoff = ((size_t)b * H + (row_ok ? iy : 0)) * W;
+    const __amdgpu_buffer_rsrc_t rx = rsrc(a.x + ((size_t)b * H + (row_ok ? iy : 0)) * W * kC, row_ok ? row_bytes : 0u);
 #pragma unroll
     for (int m = 0; m < 3; ++m) {
       if (m >= npiece) break;
-      const int ix = 32 * g - 1 + dma_lc[m];
-      const bool ok = row_ok && (unsigned)ix < (unsigned)W;
-      const float* src = ok ? a.x + (rowoff + ix) * kC + dma_ch[m] : g_wino_zero;
-      glds16(src, lds_addr(ring + ((size_t)s * kRowEntries + (wave + 4 * m) * 64) * 16));
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rx, (lds_ptr)(ring + ((size_t)s * kRowEntries + (wave + 4 * m) * 64) * 16), 16, vo[m], 0, 0, 0);
     }
   };
 
@@ -257,6 +269,7 @@ __global__ __launch_bounds__(256, 1) void conv_wino_kernel(const WinoArgs a) {
     int b, g, ty0, ty1;  // tile rows [ty0, ty1) of column group g of image b; empty = no chunk
   };
   auto decode = [&](int ch) -> Pos {  // once per chunk (two scalar divisions)
+    ch = __builtin_amdgcn_readfirstlane(ch);  // an LDS word: make it provably uniform
     Pos p{0, 0, 0, 0};
     if (ch < a.nchunks) {
       const int col = ch / a.chunks_per_col;
@@ -279,14 +292,33 @@ __global__ __launch_bounds__(256, 1) void conv_wino_kernel(const WinoArgs a) {
   Pos nnp{0, 0, 0, 0};
   int ntaken = 2;
 
-  const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc((void*)a.y, (short)0, (int)a.y_bytes, kRsrcFlags);
-  const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc((void*)a.res, (short)0, (int)a.res_bytes, kRsrcFlags);
-  const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc((void*)a.pool, (short)0, (int)a.pool_bytes, kRsrcFlags);
-  h2v mxh = {(_Float16)0.f, (_Float16)0.f};  // max |hi| of every split value (overflow check)
+  // overflow check: 0 * (pre-activation output) summed over every output; a transformed input
+  // >= 65520 rounds to an infinite hi part whose products reach the outputs as inf / NaN
+  float chk = 0.f;
+  // the lane's output byte offsets within an item's 2-row band of column group g, and within a
+  // pooled row (past the band for columns outside the image)
+  const int cbase = 16 * wave + 4 * o;
+  const int Hp = H >> 1, Wp = W >> 1;
+  unsigned yo[2][2], po = 0;
+  auto out_offsets = [&](int g) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int ox = 32 * g + 2 * t + j;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) yo[i][j] = ox < W ? (unsigned)((i * W + ox) * kC + cbase) * 4u : kOob;
+    }
+    if constexpr (POST == kPostPool) {
+      const int px = 16 * g + t;
+      po = px < Wp ? (unsigned)(px * kC + cbase) * 4u : kOob;
+    }
+  };
+  unsigned vo_cur[3];
 
   if (cur.ty0 < cur.ty1) {
     // first item of the block: its whole 4-row window into ring slots 0..3
-    for (int i = 0; i < 4; ++i) stage_row(cur.b, cur.g, 2 * cur.ty0 - 1 + i, i);
+    row_offsets(cur.g, vo_cur);
+    out_offsets(cur.g);
+    for (int i = 0; i < 4; ++i) stage_row(cur.b, 2 * cur.ty0 - 1 + i, i, vo_cur);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     int ty = cur.ty0;
@@ -299,91 +331,125 @@ __global__ __launch_bounds__(256, 1) void conv_wino_kernel(const WinoArgs a) {
       const int nty = cont ? ty + 1 : nxt.ty0;
       const bool nvalid = cont || nxt.ty0 < nxt.ty1;
       const int nbase = (base + (cont ? 2 : 4)) & (kRing - 1);
-      if (nvalid) {
-        for (int i = cont ? 2 : 0; i < 4; ++i) stage_row(np.b, np.g, 2 * nty - 1 + i, (nbase + i) & (kRing - 1));
-      }
+      // the next item's new input rows (2, or 4 after a chunk change), issued between the MFMA
+      // blocks of the k-loop (k-th pair of rows at point k) where their issue cost overlaps them
+      auto stage_next = [&](int k) {
+        if (!nvalid) return;
+        if (k == 0 && cont) return;
+        const int i0 = 2 * k;
+        if (cont) {
+          for (int i = i0; i < i0 + 2; ++i) stage_row(np.b, 2 * nty - 1 + i, (nbase + i) & (kRing - 1), vo_cur);
+        } else {
+          unsigned vo[3];
+          row_offsets(np.g, vo);
+          for (int i = i0; i < i0 + 2; ++i) stage_row(np.b, 2 * nty - 1 + i, (nbase + i) & (kRing - 1), vo);
+        }
+      };
       if (first && tid == 0) sq[2 + (ntaken & 1)] = take(ntaken);  // chunk after next
 
-      // this lane's 4 output pixels in the finishing pass (channels 16 wave + 4 o .. +3); the
+      // this lane's 4 output pixels in the finishing pass (channels 16 wave + 4 o .. +3): one
+      // descriptor per item over its 2-row band (1 row at an odd image's last tile row); the
       // residual is loaded now so its latency hides behind the k-loop
-      const int oy0 = 2 * ty, ox0 = 32 * cur.g + 2 * t;
-      const int cbase = 16 * wave + 4 * o;
-      unsigned off[2][2];
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const int oy = oy0 + i, ox = ox0 + j;
-          const bool ok = oy < H && ox < W;
-          off[i][j] = ok ? ((unsigned)((cur.b * H + oy) * W + ox) * (unsigned)kC + (unsigned)cbase) * 4u : kOob;
-        }
+      const size_t band = ((size_t)cur.b * H + 2 * ty) * W * kC;
+      const unsigned band_bytes = (2 * ty + 1 < H ? 2u : 1u) * row_bytes;
+      const __amdgpu_buffer_rsrc_t ry = rsrc(a.y + band, band_bytes);
       f32x4 rv[2][2];
       if constexpr (RES) {
+        const __amdgpu_buffer_rsrc_t rr = rsrc(a.res + band, band_bytes);
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
           for (int j = 0; j < 2; ++j)
-            rv[i][j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rr, off[i][j], 0, 0));
+            rv[i][j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rr, yo[i][j], 0, 0));
       }
 
       // ---- k-loop: 2 steps of 32 input channels, 48 MFMAs each
       f32x4 acc[4][4], cor[4][4];
       const char* rowa = ring + (size_t)((base + ra) & (kRing - 1)) * kRowEntries * 16;
       const char* rowb = ring + (size_t)((base + rb) & (kRing - 1)) * kRowEntries * 16;
+      // software-pipelined: the next k-step's LDS reads and transform sit between this k-step's
+      // MFMA blocks (source order is issue order around the asm blocks)
+      auto read_raw = [&](int kk, int hh, float4 (&da)[4], float4 (&db)[4]) {
+        // patch columns 0..3 of tile t: slots t, 17 + t, t + 1, 18 + t (even / odd column halves)
+        const int e0 = ((8 * kk + 2 * o + hh) * kSlots + t) * 16;
+        da[0] = *reinterpret_cast<const float4*>(rowa + e0);
+        da[1] = *reinterpret_cast<const float4*>(rowa + e0 + 17 * 16);
+        da[2] = *reinterpret_cast<const float4*>(rowa + e0 + 16);
+        da[3] = *reinterpret_cast<const float4*>(rowa + e0 + 18 * 16);
+        db[0] = *reinterpret_cast<const float4*>(rowb + e0);
+        db[1] = *reinterpret_cast<const float4*>(rowb + e0 + 17 * 16);
+        db[2] = *reinterpret_cast<const float4*>(rowb + e0 + 16);
+        db[3] = *reinterpret_cast<const float4*>(rowb + e0 + 18 * 16);
+      };
+      auto transform = [&](const float4 (&da)[4], const float4 (&db)[4], int hh, float (&v)[4][8]) {
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        float v[4][8];  // V[r][q] for the 8 channels of this lane
+        for (int c = 0; c < 4; ++c) {
+          float e[4];
 #pragma unroll
-        for (int hh = 0; hh < 2; ++hh) {
-          // patch columns 0..3 of tile t: slots t, 17 + t, t + 1, 18 + t (even / odd column halves)
-          const int e0 = ((8 * kk + 2 * o + hh) * kSlots + t) * 16;
-          const float4 a0 = *reinterpret_cast<const float4*>(rowa + e0);
-          const float4 a1 = *reinterpret_cast<const float4*>(rowa + e0 + 17 * 16);
-          const float4 a2 = *reinterpret_cast<const float4*>(rowa + e0 + 16);
-          const float4 a3 = *reinterpret_cast<const float4*>(rowa + e0 + 18 * 16);
-          const float4 b0 = *reinterpret_cast<const float4*>(rowb + e0);
-          const float4 b1 = *reinterpret_cast<const float4*>(rowb + e0 + 17 * 16);
-          const float4 b2 = *reinterpret_cast<const float4*>(rowb + e0 + 16);
-          const float4 b3 = *reinterpret_cast<const float4*>(rowb + e0 + 18 * 16);
-          const float4 da[4] = {a0, a1, a2, a3}, db[4] = {b0, b1, b2, b3};
-#pragma unroll
-          for (int c = 0; c < 4; ++c) {
-            float e[4];
-#pragma unroll
-            for (int jj = 0; jj < 4; ++jj) {
-              float xa = da[jj][c], xb = db[jj][c];
-              if constexpr (IOP == FVC_IN_RELU) {
-                xa = relu1(xa);
-                xb = relu1(xb);
-              }
-              e[jj] = fmaf(sb, xb, xa);
+          for (int jj = 0; jj < 4; ++jj) {
+            float xa = da[jj][c], xb = db[jj][c];
+            if constexpr (IOP == FVC_IN_RELU) {
+              xa = relu1(xa);
+              xb = relu1(xb);
             }
-            v[0][4 * hh + c] = e[0] - e[2];
-            v[1][4 * hh + c] = e[1] + e[2];
-            v[2][4 * hh + c] = e[2] - e[1];
-            v[3][4 * hh + c] = e[1] - e[3];
+            e[jj] = fmaf(sb, xb, xa);
           }
+          v[0][4 * hh + c] = e[0] - e[2];
+          v[1][4 * hh + c] = e[1] + e[2];
+          v[2][4 * hh + c] = e[2] - e[1];
+          v[3][4 * hh + c] = e[1] - e[3];
         }
-        h8 vh[4], vl[4];
+      };
+      auto split_all = [&](const float (&v)[4][8], h8 (&vh)[4], h8 (&vl)[4]) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           unsigned hw[4], lw[4];
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             split2(v[q][2 * i], v[q][2 * i + 1], hw[i], lw[i]);
-            mxh = __builtin_elementwise_max(mxh, __builtin_elementwise_abs(__builtin_bit_cast(h2v, hw[i])));
           }
           vh[q] = __builtin_bit_cast(h8, v4u{hw[0], hw[1], hw[2], hw[3]});
           vl[q] = __builtin_bit_cast(h8, v4u{lw[0], lw[1], lw[2], lw[3]});
         }
+      };
+      auto mfma_q1 = [&](int q, const h8 (&vh)[4], const h8 (&vl)[4]) {  // k-step 1 of position q
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
+        for (int n = 0; n < 4; ++n) {
+          if (n == 0 || kAllNop) wino_mfma3<false, true>(acc[q][n], cor[q][n], u[q][n][1][0], u[q][n][1][1], vh[q], vl[q]);
+          else wino_mfma3<false, false>(acc[q][n], cor[q][n], u[q][n][1][0], u[q][n][1][1], vh[q], vl[q]);
+        }
+      };
+      float4 da[4], db[4];
+      float v0[4][8], v1[4][8];
+      h8 vh0[4], vl0[4], vh1[4], vl1[4];
+      read_raw(0, 0, da, db);
+      transform(da, db, 0, v0);
+      read_raw(0, 1, da, db);
+      transform(da, db, 1, v0);
+      split_all(v0, vh0, vl0);
+      // the next k-step's transform first (its LDS reads were issued ahead), then kk = 0's 16
+      // MFMA blocks, each carrying the split of one pair of the next k-step's 32 values
+      read_raw(1, 0, da, db);
+      transform(da, db, 0, v1);
+      read_raw(1, 1, da, db);
+      stage_next(0);
+      transform(da, db, 1, v1);
+      unsigned hw1[4][4], lw1[4][4];
 #pragma unroll
-          for (int n = 0; n < 4; ++n) {
-            if (kk == 0) wino_mfma3<true>(acc[q][n], cor[q][n], u[q][n][kk][0], u[q][n][kk][1], vh[q], vl[q]);
-            else wino_mfma3<false>(acc[q][n], cor[q][n], u[q][n][kk][0], u[q][n][kk][1], vh[q], vl[q]);
-          }
+      for (int q = 0; q < 4; ++q) {
+#pragma unroll
+        for (int n = 0; n < 4; ++n)
+          ((q == 0 && n == 0) || kAllNop ? wino_mfma3_split<true> : wino_mfma3_split<false>)(acc[q][n], cor[q][n], u[q][n][0][0], u[q][n][0][1], vh0[q], vl0[q], v1[n][2 * q],
+                           v1[n][2 * q + 1], hw1[n][q], lw1[n][q]);
+        if (q == 1) stage_next(1);
       }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        vh1[q] = __builtin_bit_cast(h8, v4u{hw1[q][0], hw1[q][1], hw1[q][2], hw1[q][3]});
+        vl1[q] = __builtin_bit_cast(h8, v4u{lw1[q][0], lw1[q][1], lw1[q][2], lw1[q][3]});
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) mfma_q1(q, vh1, vl1);
       wino_mfma_drain(acc, cor);
 
       // ---- column combination Z[r][j] = sum_q M[r][q] A[q][j] (M in units of 2^kw: the scale is
@@ -424,6 +490,7 @@ __global__ __launch_bounds__(256, 1) void conv_wino_kernel(const WinoArgs a) {
 #pragma unroll
           for (int c = 0; c < 4; ++c) {
             const float ys = i == 0 ? (z[0][j][c] + z[1][j][c]) + z[2][j][c] : (z[1][j][c] - z[2][j][c]) - z[3][j][c];
+            chk = fmaf(ys, 0.f, chk);
             float tv = fmaf(ys, a.osc, bj[c]);
             if constexpr (ACT == FVC_ACT_RELU) tv = relu1(tv);
             if constexpr (ACT == FVC_ACT_LRELU) tv = fmaxf(tv, 0.1f * tv);
@@ -431,17 +498,14 @@ __global__ __launch_bounds__(256, 1) void conv_wino_kernel(const WinoArgs a) {
             vv[c] = tv;
           }
           yv[i][j] = vv;
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, vv), ry, off[i][j], 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, vv), ry, yo[i][j], 0, 0);
         }
       if constexpr (POST == kPostPool) {
         f32x4 pv;
 #pragma unroll
         for (int c = 0; c < 4; ++c) pv[c] = (((yv[0][0][c] + yv[0][1][c]) + yv[1][0][c]) + yv[1][1][c]) / 4.f;
-        const int Hp = H >> 1, Wp = W >> 1;
-        const int py = ty, px = 16 * cur.g + t;
-        const unsigned po = (py < Hp && px < Wp)
-                                ? ((unsigned)((cur.b * Hp + py) * Wp + px) * (unsigned)kC + (unsigned)cbase) * 4u
-                                : kOob;
+        const __amdgpu_buffer_rsrc_t rp =
+            rsrc(a.pool + ((size_t)cur.b * Hp + ty) * Wp * kC, ty < Hp ? (unsigned)Wp * kC * 4u : 0u);
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, pv), rp, po, 0, 0);
       }
 
@@ -451,6 +515,8 @@ __global__ __launch_bounds__(256, 1) void conv_wino_kernel(const WinoArgs a) {
         cur = nxt;
         nxt = nnp;
         ++ntaken;
+        row_offsets(cur.g, vo_cur);
+        out_offsets(cur.g);
       }
       ty = nty;
       base = nbase;
@@ -458,8 +524,7 @@ __global__ __launch_bounds__(256, 1) void conv_wino_kernel(const WinoArgs a) {
     }
   }
   {
-    const float mx = fmaxf((float)mxh[0], (float)mxh[1]);
-    if (!(mx < 65000.f) && a.ovf) atomicOr(a.ovf, 1);
+    if (chk != 0.f && a.ovf) atomicOr(a.ovf, 1);
   }
   if (a.sched && tid == 0) {
     __threadfence();
@@ -517,18 +582,9 @@ static int run_wino(const float* x, const void* upack, float osc, const float* b
   if (!x || !upack || !bias || !y || batch <= 0 || h <= 0 || w <= 0 || cu_reserve < 0 || sched_len < 0)
     return FVC_EINVAL;
   if (in_op != FVC_IN_NONE && in_op != FVC_IN_RELU) return FVC_EINVAL;
-  const unsigned long long img = (unsigned long long)h * w * kC * 4ull;
-  const unsigned long long lim = (1ull << 32) - 4096;
-  if ((unsigned long long)batch * img >= lim) {
-    // y / res / pool through 32-bit buffer offsets: split the batch
-    if (batch == 1) return FVC_EINVAL;
-    const int b1 = batch / 2;
-    const size_t xs = (size_t)h * w * kC, ps = (size_t)(h / 2) * (w / 2) * kC;
-    int rc = run_wino(x, upack, osc, bias, res, y, pool, b1, h, w, in_op, act, cu_reserve, ovf, sched, sched_len, s);
-    if (rc) return rc;
-    return run_wino(x + b1 * xs, upack, osc, bias, res ? res + b1 * xs : nullptr, y + b1 * xs,
-                    pool ? pool + b1 * ps : nullptr, batch - b1, h, w, in_op, act, cu_reserve, ovf, sched, sched_len, s);
-  }
+  // every buffer descriptor spans one input row or one 2-row output band: 32-bit offsets hold
+  // for any batch, only a band must stay below 4 GB
+  if ((unsigned long long)w * kC * 4ull * 2ull >= (1ull << 31)) return FVC_EINVAL;
   WinoArgs a;
   a.x = x;
   a.u = (const uint4*)upack;
@@ -545,10 +601,6 @@ static int run_wino(const float* x, const void* upack, float osc, const float* b
   a.nchunks = batch * a.ngroups * a.chunks_per_col;
   a.osc = osc;
   a.osc_c = osc * (1.0f / 2048.f);
-  a.y_bytes = (unsigned)(batch * img);
-  a.res_bytes = res ? (unsigned)(batch * img) : 0u;
-  a.pool_bytes = pool ? (unsigned)((unsigned long long)batch * (h / 2) * (w / 2) * kC * 4ull) : 0u;
-  a.x_bytes = (unsigned)(batch * img);
   a.ovf = ovf;
   const int reserve = env_int("FVC_X3_RESERVE", -1) >= 0 ? env_int("FVC_X3_RESERVE", 0) : cu_reserve;
   const int ncu = wino_num_cus() - (reserve < wino_num_cus() / 2 ? reserve : wino_num_cus() / 2);
