@@ -88,9 +88,15 @@ struct WinoArgs {
 
 typedef __attribute__((address_space(3))) void* lds_ptr;
 
-// a raw buffer descriptor over [p, p + bytes): offsets at or past `bytes` read 0 / drop the store
+// a raw buffer descriptor over [p, p + bytes): offsets at or past `bytes` read 0 / drop the store.
+// The inputs go through readfirstlane (free on values already in SGPRs): the compiler must see the
+// descriptor as uniform or it wraps every access in a waterfall loop (cdna_hip_programming.md T20).
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, unsigned bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, (int)bytes, kRsrcFlags);
+  const unsigned long long v = (unsigned long long)(uintptr_t)p;
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
+  void* const q = (void*)(uintptr_t)(((unsigned long long)hi << 32) | lo);
+  return __builtin_amdgcn_make_buffer_rsrc(q, (short)0, (int)__builtin_amdgcn_readfirstlane(bytes), kRsrcFlags);
 }
 
 // The three split-precision products of one (position, 16-channel N-tile) pair:
