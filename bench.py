@@ -318,7 +318,7 @@ class GpuGopJob:
         r = {"conv": timer.collect(), "x3": timer.collect(x3=True), "x3_bytes": timer.collect_bytes(x3=True),
              "hbm": timer.collect_hbm(),
              "family": {f: (timer.collect(x3=True, family=f), timer.collect_bytes(x3=True, family=f))
-                        for f in ("x3", "wino")}}
+                        for f in ("x3", "dx", "wino")}}
         if self.args.breakdown:
             for k, (n, ms, fl) in sorted(timer.breakdown().items(), key=lambda kv: -kv[1][1]):
                 print(f"{k:40s} n={n:5d} ms={ms:9.2f} TF/s={fl / (ms * 1e-3) / 1e12:7.2f}", file=sys.stderr)
@@ -470,7 +470,8 @@ def roofline_fields(prof, job, args):
                      "algorithmic_bytes_per_launch": round(x3_bytes / x3_launch) if x3_launch else None,
                      "algorithmic_gbps": round(x3_bytes / (x3_ms * 1e-3) / 1e9, 1) if x3_ms else None,
                      "kernel": "split-precision conv kernels (every conv launch but 4 small-cin layers): "
-                               "conv_x3_kernel (fp16x3 implicit-GEMM conv/deconv) + conv_wino_kernel (Winograd "
+                               "conv_x3_kernel (fp16x3 implicit-GEMM conv/deconv) + conv_dx_kernel (stride-2 "
+                               "transposed convs, all parity classes per staged tile) + conv_wino_kernel (Winograd "
                                "F(2x2,3x3) for the 64->64 3x3 layers), all their launches",
                      "achieved_is": "algorithmic fp32-conv FLOP (2 x MAC of the direct convolution) / kernel time; "
                                     "the direct kernel issues 3 f16 MFMAs per MAC (ceiling peak/3), the Winograd "
@@ -494,11 +495,12 @@ def roofline_fields(prof, job, args):
 
 
 def per_kernel_fields(prof, nfr):
-    """The roofline object split by kernel: algorithmic TF/s, launches and time of conv_x3_kernel
-    and conv_wino_kernel, and for Winograd the f16 matrix rate it actually issues (3 MFMAs per
+    """The roofline object split by kernel: algorithmic TF/s, launches and time of conv_x3_kernel,
+    conv_dx_kernel and conv_wino_kernel, and for Winograd the f16 matrix rate it actually issues (3 MFMAs per
     16/36 of a direct MAC)."""
     out = {}
-    for fam, name, mac_frac in (("x3", "conv_x3_kernel", 1.0), ("wino", "conv_wino_kernel", 16.0 / 36.0)):
+    for fam, name, mac_frac in (("x3", "conv_x3_kernel", 1.0), ("dx", "conv_dx_kernel", 1.0),
+                                ("wino", "conv_wino_kernel", 16.0 / 36.0)):
         (ms, fl, n), nbytes = prof["family"][fam]
         if not n:
             continue

@@ -25,6 +25,7 @@ _SIGS = {
     "fvc_conv2d_nhwc_f32": (c_int, [vp, vp, vp, vp, vp] + [c_int] * 10 + [vp]),
     "fvc_deconv2d_nhwc_f32": (c_int, [vp, vp, vp, vp, vp] + [c_int] * 10 + [vp]),
     "fvc_conv_x3_supported": (c_int, [c_int] * 5),
+    "fvc_deconv_x3_all_classes": (c_int, [c_int] * 4),
     "fvc_conv_x3_wpack_bytes": (c_size_t, [c_int] * 5),
     "fvc_conv_x3_pack_weight": (c_int, [vp, vp, vp] + [c_int] * 5),
     "fvc_conv2d_nhwc_x3": (c_int, [vp, vp, c_float, vp, vp, vp] + [c_int] * 11 + [vp, vp, c_int, vp]),
@@ -42,6 +43,10 @@ _SIGS = {
     "fvc_conv_wino_wpack_bytes": (c_size_t, []),
     "fvc_conv_wino_pack_weight": (c_int, [vp, vp, vp]),
     "fvc_conv2d_nhwc_wino": (c_int, [vp, vp, c_float, vp, vp, vp, vp] + [c_int] * 6 + [vp, vp, c_int, vp]),
+    "fvc_wino_tap_wpack_bytes": (c_size_t, [c_int]),
+    "fvc_wino_tap_pack_weight": (c_int, [vp, vp, vp, c_int]),
+    "fvc_conv2d_nhwc_wino_tap": (c_int, [vp, vp, c_float, vp, vp, vp] + [c_int] * 4 + [vp, c_float, c_int, c_int, vp, vp,
+                                                                                      c_int, vp]),
     "fvc_nchw_to_nhwc": (c_int, [vp, vp, c_int, c_int, c_int, c_int, c_int, vp]),
     "fvc_nhwc_to_nchw": (c_int, [vp, vp, c_int, c_int, c_int, c_int, c_int, c_int, vp]),
     "fvc_avgpool2_nhwc": (c_int, [vp, vp, c_int, c_int, c_int, c_int, vp]),

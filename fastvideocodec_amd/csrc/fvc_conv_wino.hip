@@ -69,6 +69,7 @@ constexpr bool kAllNop = FVC_WINO_ALLNOP;  // every MFMA block opens with s_nop 
 constexpr unsigned kOob = 0xFFFFFF00u;
 constexpr int kRsrcFlags = 0x00020000;
 constexpr int kPostPool = 1;
+constexpr int kPostTap = 2;
 
 
 struct WinoArgs {
@@ -84,6 +85,11 @@ struct WinoArgs {
   float osc, osc_c;      // 2^-kw, 2^-kw-11
   int* sched;            // [0] blocks finished, [1] next chunk; zero on entry, reset by the last block
   int* ovf;
+  // kPostTap: y receives P [B][H][W][pcp] = T . y per pixel (the next layer's tap partials, T
+  // [np <= 32][64] packed by fvc_wino_tap_pack_weight, scaled by 2^kt)
+  const uint4* tw;
+  float tosc, tosc_c;    // 2^-kt, 2^-kt-11
+  int pcp;
 };
 
 typedef __attribute__((address_space(3))) void* lds_ptr;
@@ -301,6 +307,7 @@ __global__ __launch_bounds__(256, 1) void conv_wino_kernel(const WinoArgs a) {
   // overflow check: 0 * (pre-activation output) summed over every output; a transformed input
   // >= 65520 rounds to an infinite hi part whose products reach the outputs as inf / NaN
   float chk = 0.f;
+  float mxy = 0.f;  // kPostTap: max |y| (y is split into fp16 halves for the tap GEMM)
   // the lane's output byte offsets within an item's 2-row band of column group g, and within a
   // pooled row (past the band for columns outside the image)
   const int cbase = 16 * wave + 4 * o;
@@ -357,8 +364,11 @@ __global__ __launch_bounds__(256, 1) void conv_wino_kernel(const WinoArgs a) {
       // descriptor per item over its 2-row band (1 row at an odd image's last tile row); the
       // residual is loaded now so its latency hides behind the k-loop
       const size_t band = ((size_t)cur.b * H + 2 * ty) * W * kC;
-      const unsigned band_bytes = (2 * ty + 1 < H ? 2u : 1u) * row_bytes;
-      const __amdgpu_buffer_rsrc_t ry = rsrc(a.y + band, band_bytes);
+      const unsigned band_rows = 2 * ty + 1 < H ? 2u : 1u;
+      const unsigned band_bytes = band_rows * row_bytes;
+      const __amdgpu_buffer_rsrc_t ry =
+          POST == kPostTap ? rsrc(a.y + ((size_t)cur.b * H + 2 * ty) * W * a.pcp, band_rows * (unsigned)W * a.pcp * 4u)
+                           : rsrc(a.y + band, band_bytes);
       f32x4 rv[2][2];
       if constexpr (RES) {
         const __amdgpu_buffer_rsrc_t rr = rsrc(a.res + band, band_bytes);
@@ -504,7 +514,8 @@ __global__ __launch_bounds__(256, 1) void conv_wino_kernel(const WinoArgs a) {
             vv[c] = tv;
           }
           yv[i][j] = vv;
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, vv), ry, yo[i][j], 0, 0);
+          if constexpr (POST != kPostTap)
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, vv), ry, yo[i][j], 0, 0);
         }
       if constexpr (POST == kPostPool) {
         f32x4 pv;
@@ -513,6 +524,60 @@ __global__ __launch_bounds__(256, 1) void conv_wino_kernel(const WinoArgs a) {
         const __amdgpu_buffer_rsrc_t rp =
             rsrc(a.pool + ((size_t)cur.b * Hp + ty) * Wp * kC, ty < Hp ? (unsigned)Wp * kC * 4u : 0u);
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, pv), rp, po, 0, 0);
+      }
+      if constexpr (POST == kPostTap) {
+        // y never reaches HBM: each wave parks its 16 channels of the item's 64 pixels in its own
+        // planes of this item's Z buffer (no other wave read them), then wave v multiplies the
+        // 64-channel y of pixel (i, j) = (v >> 1, v & 1) of the 16 tiles with the next layer's tap
+        // weights: P [16 partials x 16 tiles] per row tile on v_mfma_f32_16x16x32_f16, split
+        // precision (main = T_hi y_hi, corr = T_lo y_hi + T_hi y_lo), P = main 2^-kt + corr 2^-kt-11.
+        // Z(zb) is next written two items later, behind the next item's barrier.
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            *reinterpret_cast<f32x4*>(zw + ((i * 2 + j) * 4 + wave) * 1024 + lane * 16) = yv[i][j];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) mxy = fmaxf(mxy, fabsf(yv[i][j][c]));
+          }
+        __syncthreads();
+        const int pi = wave >> 1, pj = wave & 1;
+        h8 th[2], tl[2];
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+          // B operand: lane (t, q = lane >> 4) holds channels 32 kk + 8 q .. + 7 of tile t = quads
+          // 2 (q & 1), +1 of wave 2 kk + (q >> 1)
+          const char* src = zw + ((pi * 2 + pj) * 4 + 2 * kk + (lane >> 5)) * 1024 + ((2 * ((lane >> 4) & 1)) * 16 + t) * 16;
+          const f32x4 q0 = *reinterpret_cast<const f32x4*>(src);
+          const f32x4 q1 = *reinterpret_cast<const f32x4*>(src + 256);
+          unsigned hw[4], lw[4];
+          split2(q0[0], q0[1], hw[0], lw[0]);
+          split2(q0[2], q0[3], hw[1], lw[1]);
+          split2(q1[0], q1[1], hw[2], lw[2]);
+          split2(q1[2], q1[3], hw[3], lw[3]);
+          th[kk] = __builtin_bit_cast(h8, v4u{hw[0], hw[1], hw[2], hw[3]});
+          tl[kk] = __builtin_bit_cast(h8, v4u{lw[0], lw[1], lw[2], lw[3]});
+        }
+        const int ox = 32 * cur.g + 2 * t + pj;
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt) {
+          f32x4 pa = {0.f, 0.f, 0.f, 0.f}, pc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int kk = 0; kk < 2; ++kk) {
+            const uint4* const tw = a.tw + (size_t)((rt * 2 + kk) * 2) * 64 + lane;
+            const h8 wh = __builtin_bit_cast(h8, tw[0]);
+            const h8 wl = __builtin_bit_cast(h8, tw[64]);
+            pa = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, th[kk], pa, 0, 0, 0);
+            pc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl, th[kk], pc, 0, 0, 0);
+            pc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, tl[kk], pc, 0, 0, 0);
+          }
+          const int p0 = rt * 16 + 4 * (lane >> 4);
+          f32x4 o;
+#pragma unroll
+          for (int c = 0; c < 4; ++c) o[c] = fmaf(pc[c], a.tosc_c, pa[c] * a.tosc);
+          const unsigned so = (ox < W && p0 < a.pcp) ? (unsigned)((pi * W + ox) * a.pcp + p0) * 4u : kOob;
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, o), ry, so, 0, 0);
+        }
       }
 
       // ---- advance
@@ -530,7 +595,7 @@ __global__ __launch_bounds__(256, 1) void conv_wino_kernel(const WinoArgs a) {
     }
   }
   {
-    if (chk != 0.f && a.ovf) atomicOr(a.ovf, 1);
+    if ((chk != 0.f || !(mxy < 65000.f)) && a.ovf) atomicOr(a.ovf, 1);
   }
   if (a.sched && tid == 0) {
     __threadfence();
@@ -572,6 +637,7 @@ static int wino_launch4(const WinoArgs& a, int grid, hipStream_t s) {
 // without the pool), plus no-activation / LeakyReLU plain convs for the general entry point
 template <int IOP, int POST>
 static int wino_launch(const WinoArgs& a, int act, hipStream_t s, int grid) {
+  if constexpr (POST == kPostTap && IOP != FVC_IN_NONE) return FVC_EINVAL;
   if (a.res) {
     if (act == FVC_ACT_NONE) return wino_launch4<IOP, POST, true, FVC_ACT_NONE>(a, grid, s);
     if (act == FVC_ACT_RELU) return wino_launch4<IOP, POST, true, FVC_ACT_RELU>(a, grid, s);
@@ -584,7 +650,8 @@ static int wino_launch(const WinoArgs& a, int act, hipStream_t s, int grid) {
 
 static int run_wino(const float* x, const void* upack, float osc, const float* bias, const float* res, float* y,
                     float* pool, int batch, int h, int w, int in_op, int act, int cu_reserve, int* ovf, int* sched,
-                    int sched_len, hipStream_t s) {
+                    int sched_len, hipStream_t s, const void* tw = nullptr, float tosc = 0.f, int pcp = 0) {
+  if (tw && (pool || in_op != FVC_IN_NONE || pcp <= 0 || pcp > 32 || (pcp & 3))) return FVC_EINVAL;
   if (!x || !upack || !bias || !y || batch <= 0 || h <= 0 || w <= 0 || cu_reserve < 0 || sched_len < 0)
     return FVC_EINVAL;
   if (in_op != FVC_IN_NONE && in_op != FVC_IN_RELU) return FVC_EINVAL;
@@ -608,11 +675,16 @@ static int run_wino(const float* x, const void* upack, float osc, const float* b
   a.osc = osc;
   a.osc_c = osc * (1.0f / 2048.f);
   a.ovf = ovf;
+  a.tw = (const uint4*)tw;
+  a.tosc = tosc;
+  a.tosc_c = tosc * (1.0f / 2048.f);
+  a.pcp = pcp;
   const int reserve = env_int("FVC_X3_RESERVE", -1) >= 0 ? env_int("FVC_X3_RESERVE", 0) : cu_reserve;
   const int ncu = wino_num_cus() - (reserve < wino_num_cus() / 2 ? reserve : wino_num_cus() / 2);
   int grid = ncu < a.nchunks ? ncu : a.nchunks;
   a.sched = (sched && sched_len >= 2 && env_int("FVC_X3_DYN", 1)) ? sched : nullptr;
   if (act != FVC_ACT_NONE && act != FVC_ACT_RELU && act != FVC_ACT_LRELU) return FVC_EINVAL;
+  if (tw) return wino_launch<FVC_IN_NONE, kPostTap>(a, act, s, grid);
   if (pool) {
     if (in_op == FVC_IN_NONE) return wino_launch<FVC_IN_NONE, kPostPool>(a, act, s, grid);
     return wino_launch<FVC_IN_RELU, kPostPool>(a, act, s, grid);
@@ -680,6 +752,49 @@ int fvc_conv_wino_pack_weight(const float* w, void* wp, float* osc_out) {
           }
   free(U);
   return 0;
+}
+
+size_t fvc_wino_tap_wpack_bytes(int np) { return np > 0 && np <= 32 ? (size_t)2 * 2 * 2 * 64 * 16 : 0; }
+
+// T [np][64] (row t*cout' + co of the next layer's tap-partial form) -> [row tile][k-step][hi|lo][lane]
+// 16-B fragments: lane l holds row 16 rt + (l & 15), channels 32 kk + 8 (l >> 4) + 0..7 (the
+// v_mfma_f32_16x16x32_f16 A operand), scaled by 2^kt (max |T| 2^kt in [2^13, 2^14))
+int fvc_wino_tap_pack_weight(const float* w, void* wp, float* osc_out, int np) {
+  if (!w || !wp || !osc_out || !fvc_wino_tap_wpack_bytes(np)) return FVC_EINVAL;
+  double mx = 0.0;
+  for (int i = 0; i < np * kC; ++i) mx = fabs((double)w[i]) > mx ? fabs((double)w[i]) : mx;
+  int kt = 0;
+  if (mx > 0.0 && isfinite(mx)) {
+    int e;
+    frexp(mx, &e);
+    kt = 14 - e;
+    kt = kt < -100 ? -100 : (kt > 100 ? 100 : kt);
+  }
+  const float sc = ldexpf(1.f, kt);
+  *osc_out = ldexpf(1.f, -kt);
+  _Float16* out = (_Float16*)wp;
+  for (int rt = 0; rt < 2; ++rt)
+    for (int kk = 0; kk < 2; ++kk)
+      for (int lane = 0; lane < 64; ++lane) {
+        const int r = rt * 16 + (lane & 15);
+        for (int e = 0; e < 8; ++e) {
+          const int ci = 32 * kk + 8 * (lane >> 4) + e;
+          const float v = r < np ? w[(size_t)r * kC + ci] * sc : 0.f;
+          const _Float16 hi = (_Float16)v;
+          const size_t base = ((size_t)((rt * 2 + kk) * 2) * 64 + lane) * 8;
+          out[base + e] = hi;
+          out[base + 64 * 8 + e] = (_Float16)((v - (float)hi) * 2048.f);
+        }
+      }
+  return 0;
+}
+
+int fvc_conv2d_nhwc_wino_tap(const float* x, const void* wpack, float osc, const float* bias, const float* res,
+                             float* P, int batch, int h, int w, int act, const void* tap_wpack, float tap_osc, int pcp,
+                             int cu_reserve, int* overflow_flag, int* sched, int sched_len, fvc_stream_t stream) {
+  if (!tap_wpack) return FVC_EINVAL;
+  return run_wino(x, wpack, osc, bias, res, P, nullptr, batch, h, w, FVC_IN_NONE, act, cu_reserve, overflow_flag,
+                  sched, sched_len, (hipStream_t)stream, tap_wpack, tap_osc, pcp);
 }
 
 int fvc_conv2d_nhwc_wino(const float* x, const void* wpack, float osc, const float* bias, const float* res,

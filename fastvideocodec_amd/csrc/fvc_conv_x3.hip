@@ -38,6 +38,7 @@
 //  * transposed convs: stride^2 output-parity classes, each a stride-1 conv with a tap subset;
 //  * epilogue: scale + bias, ReLU / LeakyReLU(0.1), residual add, exp; pad channels = 0.
 #include "fvc_common.h"
+#include "fvc_dx.h"
 #include <math.h>
 #include <stdlib.h>
 
@@ -797,6 +798,7 @@ __global__ __launch_bounds__(NWV * 64) void conv_x3_kernel(const X3Args a) {
 // ------------------------------------------------------------------ host-side geometry
 struct X3Cfg {
   int cinp, coutp, ntp, cc, wm, wn, nw, nclass, nchunks, th, sin, sout;
+  int dx;     // stride-2 transposed conv on fvc_deconv_x3.hip (all classes per staged tile, one chunk)
   int wl;     // weights staged in LDS by LDS-DMA (FVC_X3_WL; chosen at pack time: it can shrink cc)
   int wnmax;  // N-tiles per block the LDS weight buffers are sized for
   int ntaps[4], nks[4], oy0[4], ox0[4];
@@ -881,6 +883,36 @@ static bool x3_cfg(int cin, int cout, int ks, int stride, int transposed, X3Cfg&
       c.dxmin = c.tdx[cl][t] < c.dxmin ? c.tdx[cl][t] : c.dxmin;
       c.dxmax = c.tdx[cl][t] > c.dxmax ? c.tdx[cl][t] : c.dxmax;
     }
+  // stride-2 transposed convs with 64 / 96 / 128 input and 64 / 128 output channels: the
+  // all-classes kernel (fvc_deconv_x3.hip) when two full-channel tile buffers fit in LDS; its pack
+  // is this pack with one channel chunk. FVC_DX=0 keeps them on this kernel (at pack AND launch).
+  c.dx = 0;
+  c.wl = 0;
+  if (transposed && stride == 2 && c.nclass == 4 && env_int("FVC_DX", 1) &&
+      (c.cinp == 64 || c.cinp == 96 || c.cinp == 128) && (c.ntp == 2 || c.ntp == 4)) {
+    int maxt = 0;
+    for (int cl = 0; cl < 4; ++cl) maxt = c.ntaps[cl] > maxt ? c.ntaps[cl] : maxt;
+    const int R = c.ntp == 4 ? 2 : 4;  // 8 wave-tiles of 2 strips x 2 N-tiles per item
+    const int ir = R + (c.dymax - c.dymin), ic = 32 + (c.dxmax - c.dxmin);
+    if (maxt <= fvc_dx::kMaxTaps && fvc_dx::lds_bytes(c.cinp, fvc_dx::plane_pix(ir, ic)) <= 160 * 1024) {
+      c.dx = 1;
+      c.cc = c.cinp;
+      c.nchunks = 1;
+      c.nw = 8;
+      c.wm = 2;
+      c.wn = 2;
+      c.wnmax = 2;
+      c.th = R;
+      long long off = 0;
+      for (int cl = 0; cl < 4; ++cl) {
+        c.nks[cl] = fvc_cdiv(c.ntaps[cl] * (c.cc / 8), 2);
+        c.wcls[cl] = off;
+        off += (long long)c.nks[cl] * c.ntp * kFrag;
+      }
+      c.wtotal = off;
+      return true;
+    }
+  }
   // channel chunk: the largest of 32 / 16 / 8 dividing cinp (shrunk below if the two LDS tile
   // buffers do not fit); FVC_X3_CC overrides for experiments
   c.cc = (c.cinp % 32 == 0) ? 32 : ((c.cinp % 16 == 0) ? 16 : 8);
@@ -997,6 +1029,102 @@ static int x3_launch_cc(int nwv, int wm, int wn, int wg, int iop, int post, cons
   return FVC_EINVAL;
 }
 
+// A stride-2 transposed conv on the all-classes kernel (fvc_deconv_x3.hip): R input rows x 32
+// columns per work item, the item's (class, strip pair, N-tile pair) wave-tiles dealt to the 8 waves
+// so that SIMD partners w and w + 4 together carry an equal share of taps (largest first, to the
+// least-loaded SIMD, then to its less-loaded wave). Tap form: one strip x all 4 N-tiles per wave-tile.
+static int run_dx(const X3Cfg& c, const float* x, const void* wpack, float osc, const float* bias, const float* res,
+                  float* y, int batch, int h, int w, int cout, int in_op, int act, int post_op, int cu_reserve,
+                  int* ovf, int* sched, int sched_len, hipStream_t s, const void* tw, float tosc, int pcp,
+                  unsigned y_bytes, unsigned x_bytes) {
+  const bool tap = tw != nullptr;
+  if (tap && res) return FVC_EINVAL;
+  const int R = c.th;
+  const int wm = tap ? 1 : 2, wn = tap ? c.ntp : 2;
+  fvc_dx::DxArgs d;
+  d.x = x;
+  d.w = (const uint4*)wpack;
+  d.bias = bias;
+  d.res = res;
+  d.y = y;
+  d.post_exp = post_op == FVC_POST_EXP ? 1 : 0;
+  d.B = batch;
+  d.H = h;
+  d.W = w;
+  d.cout = cout;
+  d.coutp = c.coutp;
+  d.ntp = c.ntp;
+  d.R = R;
+  d.ir = R + (c.dymax - c.dymin);
+  d.ic = 32 + (c.dxmax - c.dxmin);
+  d.ps = fvc_dx::plane_pix(d.ir, d.ic);
+  d.dymin = c.dymin;
+  d.dxmin = c.dxmin;
+  d.inv_ic = 1.0f / (float)d.ic;
+  d.tiles_x = fvc_cdiv(w, 32);
+  d.tiles_y = fvc_cdiv(h, R);
+  const long long nitems = (long long)batch * d.tiles_x * d.tiles_y;
+  if (nitems >= (1LL << 30)) return FVC_EINVAL;
+  d.nitems = (int)nitems;
+  d.osc = osc;
+  d.osc_c = osc * (1.0f / 2048.f);
+  d.act_slope = act == FVC_ACT_RELU ? 0.f : (act == FVC_ACT_LRELU ? 0.1f : 1.f);
+  for (int cl = 0; cl < 4; ++cl) {
+    d.nks[cl] = c.nks[cl];
+    d.oy0[cl] = c.oy0[cl];
+    d.ox0[cl] = c.ox0[cl];
+    d.wcls[cl] = c.wcls[cl];
+    for (int t = 0; t <= fvc_dx::kMaxTaps; ++t)
+      d.toff[cl][t] = t < c.ntaps[cl] ? (c.tdy[cl][t] - c.dymin) * d.ic + (c.tdx[cl][t] - c.dxmin) : 0;
+  }
+  // wave-tiles, largest first
+  int wcls_[64], wm0[64], wn0[64], wcost[64], n = 0;
+  for (int cl = 0; cl < 4; ++cl)
+    for (int m0 = 0; m0 < R; m0 += wm)
+      for (int n0 = 0; n0 < c.ntp; n0 += wn) {
+        if (n >= 64) return FVC_EINVAL;
+        wcls_[n] = cl;
+        wm0[n] = m0;
+        wn0[n] = n0;
+        wcost[n] = c.ntaps[cl];
+        ++n;
+      }
+  for (int i = 1; i < n; ++i)  // stable insertion sort by cost, descending
+    for (int j = i; j > 0 && wcost[j] > wcost[j - 1]; --j) {
+      int t;
+      t = wcost[j]; wcost[j] = wcost[j - 1]; wcost[j - 1] = t;
+      t = wcls_[j]; wcls_[j] = wcls_[j - 1]; wcls_[j - 1] = t;
+      t = wm0[j]; wm0[j] = wm0[j - 1]; wm0[j - 1] = t;
+      t = wn0[j]; wn0[j] = wn0[j - 1]; wn0[j - 1] = t;
+    }
+  int simd_load[4] = {0, 0, 0, 0}, wave_load[fvc_dx::kWaves] = {0}, wave_cnt[fvc_dx::kWaves] = {0};
+  for (int wv = 0; wv < fvc_dx::kWaves; ++wv)
+    for (int j = 0; j < fvc_dx::kMaxWT; ++j) d.wt[wv][j] = -1;
+  for (int i = 0; i < n; ++i) {
+    int sm = 0;
+    for (int q = 1; q < 4; ++q) sm = simd_load[q] < simd_load[sm] ? q : sm;
+    int wv = wave_load[sm + 4] < wave_load[sm] ? sm + 4 : sm;
+    if (wave_cnt[wv] == fvc_dx::kMaxWT) wv = wv == sm ? sm + 4 : sm;
+    if (wave_cnt[wv] == fvc_dx::kMaxWT) return FVC_EINVAL;
+    d.wt[wv][wave_cnt[wv]++] = wcls_[i] | (wm0[i] << 4) | (wn0[i] << 8);
+    simd_load[sm] += wcost[i];
+    wave_load[wv] += wcost[i];
+  }
+  d.y_bytes = y_bytes;
+  d.x_bytes = x_bytes;
+  d.ovf = ovf;
+  d.tw = (const uint4*)tw;
+  d.tosc = tosc;
+  d.tosc_c = tosc * (1.0f / 2048.f);
+  d.pcp = pcp;
+  const int reserve = env_int("FVC_X3_RESERVE", -1) >= 0 ? env_int("FVC_X3_RESERVE", 0) : cu_reserve;
+  const int ncu = x3_num_cus() - (reserve < x3_num_cus() / 2 ? reserve : x3_num_cus() / 2);
+  const int grid = ncu < d.nitems ? ncu : d.nitems;
+  d.sched = (sched && sched_len >= 2 && env_int("FVC_X3_DYN", 1)) ? sched : nullptr;
+  const size_t lds = fvc_dx::lds_bytes(c.cinp, d.ps);
+  return fvc_dx::launch(d, c.cinp, wm, wn, in_op, tap, grid, lds, s);
+}
+
 // tw != null: fused tap epilogue (y receives P [batch][Ho][Wo][pcp], see kPostTap)
 static int run_x3(const float* x, const void* wpack, float osc, const float* bias, const float* res,
                   float* y, int batch, int h, int w, int cin, int cout, int ks, int stride, int transposed,
@@ -1009,10 +1137,12 @@ static int run_x3(const float* x, const void* wpack, float osc, const float* bia
     // every output channel in one wave: N-tiles 1, 2 (2 strips per wave) or 4 (1 strip); the
     // channel chunk (and so the weight pack) stays what x3_cfg chose: fewer strips only shrink LDS
     if (post_op != FVC_POST_NONE || in_op != FVC_IN_NONE || c.wl || c.ntp == 3 || c.ntp > 4 || pcp <= 0 ||
-        pcp > 32 || (pcp & 3))
+        pcp > 32 || (pcp & 3) || (c.dx && c.ntp != 4))
       return FVC_EINVAL;
-    if (c.ntp == 4) c.wm = 1;
-    c.th = c.nw * c.wm;
+    if (!c.dx) {
+      if (c.ntp == 4) c.wm = 1;
+      c.th = c.nw * c.wm;
+    }
     post_op = kPostTap;
   }
   if (pool) {
@@ -1065,6 +1195,9 @@ static int run_x3(const float* x, const void* wpack, float osc, const float* bia
   if (xbytes >= (1ull << 32) - 4096) return FVC_EINVAL;
   a.x_bytes = (unsigned)xbytes;
   a.ovf = ovf;
+  if (c.dx)
+    return run_dx(c, x, wpack, osc, bias, res, y, batch, h, w, cout, in_op, act, post_op, cu_reserve, ovf, sched,
+                  sched_len, s, tw, tosc, pcp, a.y_bytes, a.x_bytes);
   a.sin = c.sin; a.sout = c.sout; a.nclass = c.nclass; a.nchunks = c.nchunks; a.ntp = c.ntp;
   a.dymin = c.dymin; a.dxmin = c.dxmin;
   const int th = c.th;
@@ -1183,6 +1316,11 @@ int fvc_conv_x3_supported(int cin, int cout, int ksize, int stride, int transpos
   return x3_cfg(cin, cout, ksize, stride, transposed, c) ? 1 : 0;
 }
 
+int fvc_deconv_x3_all_classes(int cin, int cout, int ksize, int stride) {
+  X3Cfg c;
+  return x3_cfg(cin, cout, ksize, stride, 1, c) && c.dx ? 1 : 0;
+}
+
 size_t fvc_conv_x3_wpack_bytes(int cin, int cout, int ksize, int stride, int transposed) {
   X3Cfg c;
   if (!x3_cfg(cin, cout, ksize, stride, transposed, c)) return 0;
@@ -1265,6 +1403,7 @@ int fvc_x3_tap_pack_weight(const float* w, void* wp, float* osc_out, int np, int
 int fvc_conv_x3_tap_supported(int cin, int cout, int ksize, int stride, int transposed, int pcp) {
   X3Cfg c;
   if (!x3_cfg(cin, cout, ksize, stride, transposed, c) || c.wl || pcp <= 0 || pcp > 32 || (pcp & 3)) return 0;
+  if (c.dx) return c.ntp == 4;  // the all-classes kernel's tap form: 1 strip x 4 N-tiles
   const int wm = c.ntp == 4 ? 1 : c.wm;
   return (wm == 2 && c.ntp <= 2) || (wm == 1 && c.ntp == 4);
 }

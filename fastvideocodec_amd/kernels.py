@@ -273,6 +273,7 @@ class PackedConv:
         # per 4-frame launch (MI355X, r2). FVC_TAPSUM=0 / 2 disables / forces the tap path for
         # every eligible layer.
         self.tap = None
+        self.wino = self.dx = False
         tapsum = os.environ.get("FVC_TAPSUM", "1")
         if (precision == "x3" and cout <= 4 and ksize in (3, 5) and stride == (2 if transposed else 1)
                 and cp4(cin) % 8 == 0 and tapsum != "0" and (tapsum == "2" or (cin >= 128 and not transposed))):
@@ -294,6 +295,8 @@ class PackedConv:
             uosc = ctypes.c_float(0.0)
             _lib.call("fvc_conv_wino_pack_weight", w.data_ptr(), upack.data_ptr(), ctypes.addressof(uosc))
             self.upack, self.uosc = upack.to(device), float(uosc.value)
+        # stride-2 transposed layers on the all-classes kernel (fvc_deconv_x3.hip, conv_dx_kernel)
+        self.dx = self.x3 and transposed and bool(lib.fvc_deconv_x3_all_classes(cin, cout, ksize, stride))
         if self.x3:
             nbytes = lib.fvc_conv_x3_wpack_bytes(cin, cout, ksize, stride, int(transposed))
             packed = torch.empty(nbytes // 2, dtype=torch.float16)
@@ -363,8 +366,8 @@ class PackedConv:
             timer.records.append((ev0, ev1, profiling.conv_flops(self.cin, self.cout, self.ksize, self.stride,
                                                                  self.transposed, B, H, W),
                                   f"{'deconv' if self.transposed else 'conv'}{self.ksize}s{self.stride} "
-                                  f"{self.cin}->{self.cout} @{H}x{W}{' wino' if wino else (' x3' if self.x3 else '')}",
-                                  self.x3, nbytes, "wino" if wino else ("x3" if self.x3 else "f32")))
+                                  f"{self.cin}->{self.cout} @{H}x{W}{' wino' if wino else (' dx' if self.dx else (' x3' if self.x3 else ''))}",
+                                  self.x3, nbytes, "wino" if wino else ("dx" if self.dx else ("x3" if self.x3 else "f32"))))
         return y
 
 
@@ -407,12 +410,19 @@ class PackedConv:
                                   True, nbytes, "wino" if self.wino else "x3"))
         return y, pool
 
+    def _wino_tap(self, tap: "TapConsumer") -> bool:
+        """The Winograd kernel's tap epilogue (fvc_conv2d_nhwc_wino_tap) takes this pair;
+        FVC_WINO_TAP=0 keeps it on the direct kernel's (A/B, tests)."""
+        return (self.wino and tap.wino_wpack is not None and cp4(self.cout) == cp4(tap.cin) and
+                os.environ.get("FVC_WINO_TAP", "1") != "0")
+
     def tap_fusable(self, tap: "TapConsumer") -> bool:
         """True if this conv can run with ``tap``'s 1x1 partial GEMM fused into its epilogue
         (split-precision path, its output feeds tap's layer, every output channel in one wave)."""
         return (self.x3 and self.tap is None and cp4(self.cout) == cp4(tap.cin) and
-                bool(_lib.load().fvc_conv_x3_tap_supported(self.cin, self.cout, self.ksize, self.stride,
-                                                            int(self.transposed), tap.pcp)))
+                (self._wino_tap(tap) or
+                 bool(_lib.load().fvc_conv_x3_tap_supported(self.cin, self.cout, self.ksize, self.stride,
+                                                             int(self.transposed), tap.pcp))))
 
     def call_tap(self, x, tap: "TapConsumer", act=ACT_NONE, res=None):
         """This conv (in_op none, act, res) fused with the first half of ``tap``'s layer: returns
@@ -433,11 +443,18 @@ class PackedConv:
         if timer is not None:
             ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             ev0.record()
-        fn = "fvc_deconv2d_nhwc_x3_tap" if self.transposed else "fvc_conv2d_nhwc_x3_tap"
-        _lib.call(fn, x.data_ptr(), self.wpack.data_ptr(), self.osc, self.bias.data_ptr(), _ptr(res), P.data_ptr(),
-                  B, H, W, self.cin, self.cout, self.ksize, self.stride, act, tap.wpack.data_ptr(), tap.osc, tap.pcp,
-                  _STATE["cu_reserve"], overflow_flag(x.device).data_ptr(), sched_scratch(x.device).data_ptr(),
-                  SCHED_LEN, stream_handle())
+        wino = self._wino_tap(tap)
+        if wino:
+            _lib.call("fvc_conv2d_nhwc_wino_tap", x.data_ptr(), self.upack.data_ptr(), self.uosc, self.bias.data_ptr(),
+                      _ptr(res), P.data_ptr(), B, H, W, act, tap.wino_wpack.data_ptr(), tap.wino_osc, tap.pcp,
+                      _STATE["cu_reserve"], overflow_flag(x.device).data_ptr(), sched_scratch(x.device).data_ptr(),
+                      SCHED_LEN, stream_handle())
+        else:
+            fn = "fvc_deconv2d_nhwc_x3_tap" if self.transposed else "fvc_conv2d_nhwc_x3_tap"
+            _lib.call(fn, x.data_ptr(), self.wpack.data_ptr(), self.osc, self.bias.data_ptr(), _ptr(res), P.data_ptr(),
+                      B, H, W, self.cin, self.cout, self.ksize, self.stride, act, tap.wpack.data_ptr(), tap.osc,
+                      tap.pcp, _STATE["cu_reserve"], overflow_flag(x.device).data_ptr(),
+                      sched_scratch(x.device).data_ptr(), SCHED_LEN, stream_handle())
         if timer is not None:
             ev1.record()
             # algorithmic work: this conv + the next layer's MACs (the partial GEMM does all of them)
@@ -446,8 +463,9 @@ class PackedConv:
             nbytes = 4 * (x.numel() + P.numel() + (res.numel() if res is not None else 0)) + \
                 self.wpack.numel() * self.wpack.element_size() + tap.wpack.numel() * tap.wpack.element_size()
             timer.records.append((ev0, ev1, fl, f"{'deconv' if self.transposed else 'conv'}{self.ksize}s{self.stride} "
-                                  f"{self.cin}->{self.cout} @{H}x{W} x3 +tap{tap.ksize}x{tap.ksize}->{tap.cout}",
-                                  True, nbytes, "x3"))
+                                  f"{self.cin}->{self.cout} @{H}x{W} {'wino' if wino else ('dx' if self.dx else 'x3')} "
+                                  f"+tap{tap.ksize}x{tap.ksize}->{tap.cout}", True, nbytes,
+                                  "wino" if wino else ("dx" if self.dx else "x3")))
         return P
 
 
@@ -478,6 +496,13 @@ class TapConsumer:
         _lib.call("fvc_x3_tap_pack_weight", wt.data_ptr(), packed.data_ptr(), ctypes.addressof(osc), self.np, cin)
         self.osc = float(osc.value)
         self.wpack = packed.to(device)
+        # the same rows for the Winograd producer's tap epilogue (64-channel producers only)
+        self.wino_wpack, self.wino_osc = None, 0.0
+        if cin == 64 and lib.fvc_wino_tap_wpack_bytes(self.np):
+            wp = torch.empty(lib.fvc_wino_tap_wpack_bytes(self.np) // 2, dtype=torch.float16)
+            wosc = ctypes.c_float(0.0)
+            _lib.call("fvc_wino_tap_pack_weight", wt.data_ptr(), wp.data_ptr(), ctypes.addressof(wosc), self.np)
+            self.wino_wpack, self.wino_osc = wp.to(device), float(wosc.value)
         self.bias = bias.detach().to(device, torch.float32).contiguous()
 
     def gather(self, P, act=ACT_NONE, post=POST_NONE, res=None):

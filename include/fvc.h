@@ -104,6 +104,12 @@ int fvc_deconv2d_nhwc_x3(const float* x, const void* wpack, float osc, const flo
                          const float* res, float* y, int batch, int h, int w, int cin, int cout,
                          int ksize, int stride, int in_op, int act, int post_op, int cu_reserve,
                          int* overflow_flag, int* sched, int sched_len, fvc_stream_t stream);
+/* 1 if fvc_deconv2d_nhwc_x3 / _x3_tap run this transposed geometry on the all-classes kernel
+ * (stride 2, 64 / 96 / 128 input and 64 / 128 output channels: the four output-parity classes of a
+ * tile from one staged full-channel input tile; its pack is the x3 pack with one channel chunk).
+ * The environment variable FVC_DX=0 (read at pack and at launch time) keeps such layers on the
+ * per-class path of conv_x3_kernel. */
+int fvc_deconv_x3_all_classes(int cin, int cout, int ksize, int stride);
 /* Fused producer + tap partials of a cout <= 4 consumer (the pair nn.Conv2d(c->128/64) ->
  * nn.Conv2d(128/64->2/3): synthesis_mv.py:41-43 deconv7 -> deconv8, endecoder.py:278-279
  * Warp_net conv5 -> conv6): the producer conv / transposed conv runs as fvc_*_x3 (in_op none,
@@ -146,6 +152,18 @@ int fvc_conv2d_nhwc_wino(const float* x, const void* wpack, float osc, const flo
                          const float* res, float* y, float* pool, int batch, int h, int w, int in_op,
                          int act, int cu_reserve, int* overflow_flag, int* sched, int sched_len,
                          fvc_stream_t stream);
+/* The same Winograd conv (in_op none, act, res) fused with the next layer's tap partials, as
+ * fvc_conv2d_nhwc_x3_tap: instead of y it writes P [batch][h][w][pcp] = T . y per pixel (Warp_net
+ * conv5.conv2 -> conv6, endecoder.py:278-279: 27 partials of the 64 -> 3 3x3 conv), which
+ * fvc_tap_gather_nhwc sums into the consumer's output. T [np <= 32][64] (rows t*cout' + co) is
+ * packed by fvc_wino_tap_pack_weight (host, fvc_wino_tap_wpack_bytes(np) bytes; pcp = np rounded
+ * up to 4). */
+size_t fvc_wino_tap_wpack_bytes(int np);
+int fvc_wino_tap_pack_weight(const float* w_host, void* wpack_host, float* osc_out, int np);
+int fvc_conv2d_nhwc_wino_tap(const float* x, const void* wpack, float osc, const float* bias,
+                             const float* res, float* P, int batch, int h, int w, int act,
+                             const void* tap_wpack, float tap_osc, int pcp, int cu_reserve,
+                             int* overflow_flag, int* sched, int sched_len, fvc_stream_t stream);
 
 /* ------------------------------------------------------------------ layout / resampling */
 int fvc_nchw_to_nhwc(const float* src, float* dst, int batch, int c, int h, int w, int cp,

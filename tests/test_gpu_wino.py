@@ -155,3 +155,44 @@ def test_wino_overflow_flag(dev):
     x[0, 5, 7, 9] = 7e4
     pw(to_nhwc(x).to(dev))
     assert K.x3_overflow(reset=True)
+
+
+@pytest.mark.parametrize("shape", [(2, 19, 45), (1, 36, 98), (3, 5, 33)])
+def test_wino_tap_epilogue(dev, shape, monkeypatch):
+    """Winograd conv (residual, no activation: Warp_net conv5.conv2) with conv6's 27 tap partials in
+    its epilogue (fvc_conv2d_nhwc_wino_tap) + the gather, against float64 torch and against the
+    direct kernel's tap epilogue (FVC_WINO_TAP=0); ragged tile rows and column groups."""
+    from fastvideocodec_amd import net
+    B, H, W = shape
+    g = torch.Generator().manual_seed(40 + H)
+    x = torch.randn(B, 64, H, W, generator=g)
+    res = torch.randn(B, 64, H, W, generator=g)
+    w1 = torch.randn(64, 64, 3, 3, generator=g) * 0.04
+    b1 = torch.randn(64, generator=g) * 0.1
+    w2 = torch.randn(3, 64, 3, 3, generator=g) * (1.0 / (64 * 9) ** 0.5)
+    b2 = torch.randn(3, generator=g) * 0.1
+    y = F.conv2d(x.double(), w1.double(), b1.double(), 1, 1) + res.double()
+    ref = F.conv2d(y, w2.double(), b2.double(), 1, 1)
+    prod = net._ConvP(64, 64, 3, 1, False)
+    prod.weight.data.copy_(w1)
+    prod.bias.data.copy_(b1)
+    cons = net._ConvP(64, 3, 3, 1, False)
+    cons.weight.data.copy_(w2)
+    cons.bias.data.copy_(b2)
+    prod.to(dev)
+    cons.to(dev)
+    xd, rd = to_nhwc(x).to(dev), to_nhwc(res).to(dev)
+    t = cons.tap_consumer()
+    assert prod.packed().wino and t.wino_wpack is not None and prod.packed()._wino_tap(t)
+    K.x3_overflow(reset=True)
+    out_w = net.conv_then_tap(prod, xd, cons, res=rd)
+    monkeypatch.setenv("FVC_WINO_TAP", "0")
+    out_d = net.conv_then_tap(prod, xd, cons, res=rd)
+    torch.cuda.synchronize()
+    assert not K.x3_overflow(reset=True)
+    scale = float(ref.abs().max())
+    ew = float((from_nhwc(out_w.cpu())[:, :3].double() - ref).abs().max())
+    ed = float((from_nhwc(out_d.cpu())[:, :3].double() - ref).abs().max())
+    print(f"{shape}: wino tap err {ew / scale:.2e}, direct tap err {ed / scale:.2e} (of output scale)")
+    assert ew <= 2e-6 * scale, (ew, ed, scale)
+    assert float(out_w[..., 3:].abs().max()) == 0.0
