@@ -892,8 +892,11 @@ static bool x3_cfg(int cin, int cout, int ks, int stride, int transposed, X3Cfg&
       (c.cinp == 64 || c.cinp == 96 || c.cinp == 128) && (c.ntp == 2 || c.ntp == 4)) {
     int maxt = 0;
     for (int cl = 0; cl < 4; ++cl) maxt = c.ntaps[cl] > maxt ? c.ntaps[cl] : maxt;
-    const int R = c.ntp == 4 ? 2 : 4;  // 8 wave-tiles of 2 strips x 2 N-tiles per item
-    const int ir = R + (c.dymax - c.dymin), ic = 32 + (c.dxmax - c.dxmin);
+    // items of R input rows x sw columns: 128 channels 8 x 16 (four 2 x 16-pixel strips), fewer
+    // channels 2 x 32 (4 N-tiles) or 4 x 32 (2 N-tiles): 8 wave-tiles of 2 strips x 2 N-tiles or more
+    const int sw = fvc_dx::strip_width(c.cinp);
+    const int R = sw == 16 ? 8 : (c.ntp == 4 ? 2 : 4);
+    const int ir = R + (c.dymax - c.dymin), ic = sw + (c.dxmax - c.dxmin);
     if (maxt <= fvc_dx::kMaxTaps && fvc_dx::lds_bytes(c.cinp, fvc_dx::plane_pix(ir, ic)) <= 160 * 1024) {
       c.dx = 1;
       c.cc = c.cinp;
@@ -1040,6 +1043,8 @@ static int run_dx(const X3Cfg& c, const float* x, const void* wpack, float osc, 
   const bool tap = tw != nullptr;
   if (tap && res) return FVC_EINVAL;
   const int R = c.th;
+  const int sw = fvc_dx::strip_width(c.cinp);
+  const int S = R / (32 / sw);  // strips per item
   const int wm = tap ? 1 : 2, wn = tap ? c.ntp : 2;
   fvc_dx::DxArgs d;
   d.x = x;
@@ -1055,13 +1060,14 @@ static int run_dx(const X3Cfg& c, const float* x, const void* wpack, float osc, 
   d.coutp = c.coutp;
   d.ntp = c.ntp;
   d.R = R;
+  d.sw = sw;
   d.ir = R + (c.dymax - c.dymin);
-  d.ic = 32 + (c.dxmax - c.dxmin);
+  d.ic = sw + (c.dxmax - c.dxmin);
   d.ps = fvc_dx::plane_pix(d.ir, d.ic);
   d.dymin = c.dymin;
   d.dxmin = c.dxmin;
   d.inv_ic = 1.0f / (float)d.ic;
-  d.tiles_x = fvc_cdiv(w, 32);
+  d.tiles_x = fvc_cdiv(w, sw);
   d.tiles_y = fvc_cdiv(h, R);
   const long long nitems = (long long)batch * d.tiles_x * d.tiles_y;
   if (nitems >= (1LL << 30)) return FVC_EINVAL;
@@ -1077,39 +1083,88 @@ static int run_dx(const X3Cfg& c, const float* x, const void* wpack, float osc, 
     for (int t = 0; t <= fvc_dx::kMaxTaps; ++t)
       d.toff[cl][t] = t < c.ntaps[cl] ? (c.tdy[cl][t] - c.dymin) * d.ic + (c.tdx[cl][t] - c.dxmin) : 0;
   }
-  // wave-tiles, largest first
-  int wcls_[64], wm0[64], wn0[64], wcost[64], n = 0;
+  // wave-tiles (class, first strip, first N-tile), cost = the class's taps. Two assignments:
+  // unpaired -- largest first to the least-loaded SIMD, then to its less-loaded wave; paired -- the
+  // wave-tiles of one (class, N-tiles) in pairs of strip groups as one job on SIMD partners w and
+  // w + 4 at the same list position, so the two waves stream the same weight fragments together
+  // (one L2 read feeds both through L1). Paired is taken unless its busiest SIMD carries > 15 % more
+  // taps (FVC_DX_PAIR=0/1 forces either).
+  struct WT {
+    int cl, m0, n0, cost;
+  };
+  WT wt[64];
+  int n = 0;
   for (int cl = 0; cl < 4; ++cl)
-    for (int m0 = 0; m0 < R; m0 += wm)
-      for (int n0 = 0; n0 < c.ntp; n0 += wn) {
+    for (int n0 = 0; n0 < c.ntp; n0 += wn)
+      for (int m0 = 0; m0 < S; m0 += wm) {
         if (n >= 64) return FVC_EINVAL;
-        wcls_[n] = cl;
-        wm0[n] = m0;
-        wn0[n] = n0;
-        wcost[n] = c.ntaps[cl];
-        ++n;
+        wt[n++] = {cl, m0, n0, c.ntaps[cl]};
       }
-  for (int i = 1; i < n; ++i)  // stable insertion sort by cost, descending
-    for (int j = i; j > 0 && wcost[j] > wcost[j - 1]; --j) {
-      int t;
-      t = wcost[j]; wcost[j] = wcost[j - 1]; wcost[j - 1] = t;
-      t = wcls_[j]; wcls_[j] = wcls_[j - 1]; wcls_[j - 1] = t;
-      t = wm0[j]; wm0[j] = wm0[j - 1]; wm0[j - 1] = t;
-      t = wn0[j]; wn0[j] = wn0[j - 1]; wn0[j - 1] = t;
+  auto enc = [](const WT& t) { return t.cl | (t.m0 << 4) | (t.n0 << 8); };
+  auto by_cost = [](WT* v, int k) {  // stable insertion sort, descending
+    for (int i = 1; i < k; ++i)
+      for (int j = i; j > 0 && v[j].cost > v[j - 1].cost; --j) {
+        const WT t = v[j];
+        v[j] = v[j - 1];
+        v[j - 1] = t;
+      }
+  };
+  int up[fvc_dx::kWaves][fvc_dx::kMaxWT], upc[fvc_dx::kWaves] = {0};
+  int pp[fvc_dx::kWaves][fvc_dx::kMaxWT], ppc[fvc_dx::kWaves] = {0};
+  int up_max = 0, pp_max = 1 << 30;
+  {  // unpaired
+    WT v[64];
+    for (int i = 0; i < n; ++i) v[i] = wt[i];
+    by_cost(v, n);
+    int sl[4] = {0, 0, 0, 0}, wl[fvc_dx::kWaves] = {0};
+    for (int i = 0; i < n; ++i) {
+      int sm = 0;
+      for (int q = 1; q < 4; ++q) sm = sl[q] < sl[sm] ? q : sm;
+      int wv = wl[sm + 4] < wl[sm] ? sm + 4 : sm;
+      if (upc[wv] == fvc_dx::kMaxWT) wv = wv == sm ? sm + 4 : sm;
+      if (upc[wv] == fvc_dx::kMaxWT) return FVC_EINVAL;
+      up[wv][upc[wv]++] = enc(v[i]);
+      sl[sm] += v[i].cost;
+      wl[wv] += v[i].cost;
     }
-  int simd_load[4] = {0, 0, 0, 0}, wave_load[fvc_dx::kWaves] = {0}, wave_cnt[fvc_dx::kWaves] = {0};
-  for (int wv = 0; wv < fvc_dx::kWaves; ++wv)
-    for (int j = 0; j < fvc_dx::kMaxWT; ++j) d.wt[wv][j] = -1;
-  for (int i = 0; i < n; ++i) {
-    int sm = 0;
-    for (int q = 1; q < 4; ++q) sm = simd_load[q] < simd_load[sm] ? q : sm;
-    int wv = wave_load[sm + 4] < wave_load[sm] ? sm + 4 : sm;
-    if (wave_cnt[wv] == fvc_dx::kMaxWT) wv = wv == sm ? sm + 4 : sm;
-    if (wave_cnt[wv] == fvc_dx::kMaxWT) return FVC_EINVAL;
-    d.wt[wv][wave_cnt[wv]++] = wcls_[i] | (wm0[i] << 4) | (wn0[i] << 8);
-    simd_load[sm] += wcost[i];
-    wave_load[wv] += wcost[i];
+    for (int q = 0; q < 4; ++q) up_max = sl[q] > up_max ? sl[q] : up_max;
   }
+  if ((S / wm) % 2 == 0) {  // paired: jobs = consecutive wave-tile pairs of one (class, N-tiles)
+    WT jobs[32];
+    int nj = 0;
+    for (int i = 0; i + 1 < n; i += 2) jobs[nj++] = wt[i];  // wt[i + 1]: same class / N-tiles, next strips
+    int jidx[32];
+    for (int i = 0; i < nj; ++i) jidx[i] = i;
+    for (int i = 1; i < nj; ++i)
+      for (int j = i; j > 0 && jobs[jidx[j]].cost > jobs[jidx[j - 1]].cost; --j) {
+        const int t = jidx[j];
+        jidx[j] = jidx[j - 1];
+        jidx[j - 1] = t;
+      }
+    int sl[4] = {0, 0, 0, 0};
+    bool ok = true;
+    for (int i = 0; i < nj && ok; ++i) {
+      const int j = jidx[i];
+      int sm = 0;
+      for (int q = 1; q < 4; ++q) sm = sl[q] < sl[sm] ? q : sm;
+      if (ppc[sm] == fvc_dx::kMaxWT) {
+        ok = false;
+        break;
+      }
+      pp[sm][ppc[sm]++] = enc(wt[2 * j]);
+      pp[sm + 4][ppc[sm + 4]++] = enc(wt[2 * j + 1]);
+      sl[sm] += 2 * jobs[j].cost;
+    }
+    if (ok) {
+      pp_max = 0;
+      for (int q = 0; q < 4; ++q) pp_max = sl[q] > pp_max ? sl[q] : pp_max;
+    }
+  }
+  const int pair_env = env_int("FVC_DX_PAIR", -1);
+  const bool paired = pp_max < (1 << 30) && (pair_env == 1 || (pair_env != 0 && pp_max * 100 <= up_max * 115));
+  for (int wv = 0; wv < fvc_dx::kWaves; ++wv)
+    for (int j = 0; j < fvc_dx::kMaxWT; ++j)
+      d.wt[wv][j] = paired ? (j < ppc[wv] ? pp[wv][j] : -1) : (j < upc[wv] ? up[wv][j] : -1);
   d.y_bytes = y_bytes;
   d.x_bytes = x_bytes;
   d.ovf = ovf;

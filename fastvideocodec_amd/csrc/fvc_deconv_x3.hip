@@ -67,8 +67,10 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, unsigned b
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, kRsrcFlags);
 }
 
-template <int CIN, int WM, int WN, int IOP, bool TAP>
+template <int CIN, int WM, int WN, int IOP, bool TAP, int SW>
 __global__ __launch_bounds__(kNT) void conv_dx_kernel(const DxArgs a) {
+  static_assert(SW == 32 || SW == 16, "strip shapes: 1 x 32 or 2 x 16 input pixels");
+  constexpr int SR = 32 / SW;   // input rows per strip
   constexpr int C8 = CIN / 8;   // channel octets (LDS planes per hi / lo half)
   constexpr int KPT = C8 / 2;   // k-steps per tap (one k-step = two octets of one tap)
   static_assert(C8 % 2 == 0, "a k-step's two octets must belong to one tap");
@@ -84,6 +86,11 @@ __global__ __launch_bounds__(kNT) void conv_dx_kernel(const DxArgs a) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int li = lane & 31;
   const int lh = lane >> 5;
+  // the lane's pixel in its strip (MFMA column li): 1 x 32 strips take column li; 2 x 16 strips take
+  // row li >> 4 and, on the second row, the columns rotated by one ((li - 17) & 15) so that each
+  // 16-lane group of a ds_read_b128 hits 16 distinct bank quads with the odd row pitch of 17 pixels
+  const int sdr = SW == 32 ? 0 : (li >> 4);
+  const int sdc = SW == 32 ? li : (li < 16 ? li : ((li - 17) & 15));
   const int psh = a.ps * 8;           // halves per LDS plane
   const int tile_h = 2 * C8 * psh;    // halves per tile buffer
   const int Ho = 2 * a.H, Wo = 2 * a.W;
@@ -113,7 +120,7 @@ __global__ __launch_bounds__(kNT) void conv_dx_kernel(const DxArgs a) {
     const int r = it - b * per;
     const int ty = r / a.tiles_x;
     ty0 = ty * a.R;
-    tx0 = (r - ty * a.tiles_x) * 32;
+    tx0 = (r - ty * a.tiles_x) * SW;
   };
 
   // ---- staging: item e = (tile pixel p, octet o) -> two 16-B loads (halo pixels outside the
@@ -204,7 +211,7 @@ __global__ __launch_bounds__(kNT) void conv_dx_kernel(const DxArgs a) {
       const uint4* const wcl = a.w + a.wcls[cls] + lane;
       int pix[WM];
 #pragma unroll
-      for (int m = 0; m < WM; ++m) pix[m] = ((m0 + m) * a.ic + li) * 8;
+      for (int m = 0; m < WM; ++m) pix[m] = (((m0 + m) * SR + sdr) * a.ic + sdc) * 8;
 
       f32x16 acc[WM][WN], cor[WM][WN];
 #pragma unroll
@@ -297,11 +304,11 @@ __global__ __launch_bounds__(kNT) void conv_dx_kernel(const DxArgs a) {
       // ---- epilogue of this wave-tile: input position (row, col) of strip m, lane li ->
       // output pixel (2 row + py, 2 col + px); lane (li, lh) holds channels 8g + 4lh + {0..3}
       const int oyc = a.oy0[cls], oxc = a.ox0[cls];
-      const int col = tx0 + li;
+      const int col = tx0 + sdc;
       if constexpr (TAP) {
 #pragma unroll
         for (int m = 0; m < WM; ++m) {
-          const int row = ty0 + m0 + m;
+          const int row = ty0 + (m0 + m) * SR + sdr;
           const bool ok = row < a.H && col < a.W;
           const unsigned pixo = ((unsigned)b * Ho + 2 * row + oyc) * (unsigned)Wo + 2 * col + oxc;
           f32x16 pa, pc;
@@ -353,7 +360,7 @@ __global__ __launch_bounds__(kNT) void conv_dx_kernel(const DxArgs a) {
       } else {
 #pragma unroll
         for (int m = 0; m < WM; ++m) {
-          const int row = ty0 + m0 + m;
+          const int row = ty0 + (m0 + m) * SR + sdr;
           const bool ok = row < a.H && col < a.W;
           const unsigned pixo = ((unsigned)b * Ho + 2 * row + oyc) * (unsigned)Wo + 2 * col + oxc;
 #pragma unroll
@@ -413,10 +420,14 @@ __global__ __launch_bounds__(kNT) void conv_dx_kernel(const DxArgs a) {
 
 template <int CIN, int WM, int WN, int IOP, bool TAP>
 int launch_t(const DxArgs& a, int grid, size_t lds, hipStream_t s) {
-  const hipError_t e = hipFuncSetAttribute((const void*)conv_dx_kernel<CIN, WM, WN, IOP, TAP>,
+  // 128-channel layers: 2 x 16-pixel strips (8-row items: two full-channel buffers still fit);
+  // fewer channels: 1 x 32-pixel strips
+  constexpr int SW = CIN == 128 ? 16 : 32;
+  if (a.sw != SW) return FVC_EINVAL;
+  const hipError_t e = hipFuncSetAttribute((const void*)conv_dx_kernel<CIN, WM, WN, IOP, TAP, SW>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return -(int)e;
-  hipLaunchKernelGGL((conv_dx_kernel<CIN, WM, WN, IOP, TAP>), dim3(grid), dim3(kNT), lds, s, a);
+  hipLaunchKernelGGL((conv_dx_kernel<CIN, WM, WN, IOP, TAP, SW>), dim3(grid), dim3(kNT), lds, s, a);
   FVC_CHECK_LAUNCH();
   return 0;
 }

@@ -17,7 +17,8 @@ struct DxArgs {
   float* y;           // [B][2H][2W][coutp], or tap partials [B][2H][2W][pcp]
   int post_exp;       // exp after the residual (pad channels 0)
   int B, H, W, cout, coutp, ntp;
-  int R;              // input rows per work item (strips of 32 input columns)
+  int R;              // input rows per work item
+  int sw;             // input columns per work item = pixels per strip row (32: 1 x 32 strips, 16: 2 x 16)
   int ir, ic, ps;     // staged tile rows / columns, LDS plane stride (16-B entries, odd)
   int dymin, dxmin;
   float inv_ic;
@@ -40,6 +41,8 @@ struct DxArgs {
 __attribute__((visibility("hidden"))) size_t lds_bytes(int cinp, int ps);
 // odd plane stride >= ir * ic (conflict-free staging writes of consecutive octets)
 __attribute__((visibility("hidden"))) int plane_pix(int ir, int ic);
+// strip width of a geometry: 16 (2 x 16-pixel strips, 8-row items) for 128 input channels, else 32
+inline int strip_width(int cinp) { return cinp == 128 ? 16 : 32; }
 // cinp in {64, 96, 128}; (wm, wn) = (2, 2) plain epilogue or (1, ntp) with the tap epilogue;
 // iop in {FVC_IN_NONE, FVC_IN_ROUND}
 __attribute__((visibility("hidden"))) int launch(const DxArgs& a, int cinp, int wm, int wn, int iop, bool tap,

@@ -16,6 +16,8 @@ CASES = {
     "c7_32_64_full": (32, 64, 7, 1, False, 1088, 1920),
     "d3_128_half": (128, 128, 3, 2, True, 544, 960),
     "d3_128_quarter": (128, 128, 3, 2, True, 272, 480),
+    "d3_128_eighth": (128, 128, 3, 2, True, 136, 240),
+    "d3_128_full": (128, 128, 3, 2, True, 1088, 1920),
     "c3_128_2_full": (128, 2, 3, 1, False, 1088, 1920),
     "d5_64_quarter": (64, 64, 5, 2, True, 272, 480),
     "d5_96_64_16": (96, 64, 5, 2, True, 136, 240),

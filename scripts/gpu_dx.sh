@@ -11,7 +11,7 @@ timeout -k 10 300 python -u -m pytest tests/test_gpu_deconv.py tests/test_gpu_wi
 rc=$?
 echo "dx tests exit $rc"; grep -E "passed|failed|error|err " gpurun_out/pytest_dx_$TAG.log | tail -24
 [ $rc -eq 0 ] || exit $rc
-CASES=d3_128_half,d3_128_quarter,d5_64_quarter,d5_96_64_16
+CASES=d3_128_half,d3_128_quarter,d3_128_eighth,d5_64_quarter,d5_96_64_16
 for v in 0 1; do
   FVC_DX=$v timeout -k 10 180 python -u scripts/conv_micro.py --batch 8 --cases $CASES \
     > gpurun_out/micro_dx${v}_$TAG.txt 2>&1 || { echo "micro $v failed"; tail -20 gpurun_out/micro_dx${v}_$TAG.txt; exit 1; }

@@ -25,7 +25,8 @@ def from_nhwc(y, c):
 CASES = [
     (128, 128, 3, 2, 5, 9, K.IN_ROUND, K.ACT_LRELU, False, K.POST_NONE),   # mvDecoder deconv1 (rounded latents)
     (128, 128, 3, 1, 34, 70, K.IN_NONE, K.ACT_RELU, False, K.POST_NONE),   # 2 column groups + 6 cut columns
-    (128, 128, 3, 3, 7, 33, K.IN_RELU, K.ACT_NONE, True, K.POST_NONE),     # odd rows (half a 2-row item)
+    (128, 128, 3, 3, 7, 33, K.IN_RELU, K.ACT_NONE, True, K.POST_NONE),     # odd rows, 3 cut columns
+    (128, 128, 3, 1, 19, 47, K.IN_NONE, K.ACT_LRELU, False, K.POST_NONE),  # 8-row items cut at 3 rows
     (96, 64, 5, 2, 4, 6, K.IN_ROUND, K.ACT_NONE, False, K.POST_NONE),      # resDecoder deconv1
     (64, 64, 5, 2, 17, 30, K.IN_NONE, K.ACT_RELU, False, K.POST_NONE),     # hyperprior deconv, 17 rows
     (64, 64, 5, 1, 35, 66, K.IN_ABS, K.ACT_NONE, True, K.POST_NONE),
@@ -97,8 +98,14 @@ def test_deconv_all_classes_schedules_and_determinism(dev, monkeypatch):
     c = pc(x, act=K.ACT_RELU)
     monkeypatch.setenv("FVC_X3_RESERVE", "100")
     d = pc(x, act=K.ACT_RELU)
+    # wave-tiles paired on SIMD partners or dealt one by one: the same sums per output
+    monkeypatch.setenv("FVC_DX_PAIR", "0")
+    e = pc(x, act=K.ACT_RELU)
+    monkeypatch.setenv("FVC_DX_PAIR", "1")
+    f = pc(x, act=K.ACT_RELU)
     torch.cuda.synchronize()
     assert torch.equal(a, a2) and torch.equal(a, c) and torch.equal(a, d)
+    assert torch.equal(a, e) and torch.equal(a, f)
     assert int(K.sched_scratch(dev)[:2].abs().sum()) == 0
 
 
