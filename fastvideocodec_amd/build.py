@@ -10,7 +10,7 @@ import sys
 from concurrent.futures import ThreadPoolExecutor
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-VARIANT_SRCS = ("fvc_conv_x3.hip", "fvc_conv_wino.hip")
+VARIANT_SRCS = ("fvc_conv_x3.hip", "fvc_deconv_x3.hip", "fvc_conv_wino.hip")
 SRCS = ["fvc_conv.hip", "fvc_conv_x3.hip", "fvc_deconv_x3.hip", "fvc_conv_wino.hip", "fvc_elem.hip", "fvc_coder.hip", "fvc_iframe.hip",
         "fvc_torchac.hip"]
 # per-source flags: the Winograd transforms stay scalar f32 (packed f32 VALU issues slower beside MFMAs)
@@ -48,7 +48,7 @@ def _compile(src, verbose, extra=(), tag=""):
     os.replace(obj + ".tmp", obj)
 
 
-def build(force=False, verbose=True, variant=None, defines=()):
+def build(force=False, verbose=True, variant=None, defines=(), only=None):
     """Build libfvc.so; variant="name" with extra -D defines builds an experiment library
     libfvc_<name>.so instead (loaded with FVC_LIB_PATH; never the product)."""
     os.makedirs(OBJDIR, exist_ok=True)
@@ -57,7 +57,7 @@ def build(force=False, verbose=True, variant=None, defines=()):
     extra = [f"-D{d}" for d in defines]
     # experiment variants recompile only the conv kernels (the -D switches are theirs) and link
     # the product objects of every other source
-    vsrcs = [s for s in SRCS if not variant or s in VARIANT_SRCS]
+    vsrcs = [s for s in SRCS if not variant or (s in VARIANT_SRCS and (not only or s in only))]
     if variant:
         build(force=False, verbose=verbose)
     todo = [s for s in vsrcs if force or _stale(_obj(s, tag), [os.path.join(HERE, "csrc", s)] + HEADERS)]
@@ -80,5 +80,6 @@ if __name__ == "__main__":
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--variant", default=None)
     ap.add_argument("-D", dest="defines", action="append", default=[])
+    ap.add_argument("--only", action="append", default=None, help="variant: recompile only these sources")
     a = ap.parse_args()
-    build(force=a.force, variant=a.variant, defines=a.defines)
+    build(force=a.force, variant=a.variant, defines=a.defines, only=a.only)

@@ -37,6 +37,13 @@ constexpr int kRsrcFlags = 0x00020000;
 constexpr int kNT = 512;     // threads per block (8 waves, 2 per SIMD)
 constexpr int kFrag = 128;   // uint4 per (k-step, N-tile): hi and lo planes x 64 lanes
 constexpr int kHdr = 1024;   // LDS header: bias (512 B), staging sink, work-item queue
+// FVC_DX_KO (compile-time, experiment builds only -- wrong results): knock out parts of the item to
+// find the binding unit. bit 0: weight loads (registers), bit 1: staging of the next tile, bit 2:
+// LDS operand reads (registers), bit 3: MFMAs, bit 4: epilogue stores
+#ifndef FVC_DX_KO
+#define FVC_DX_KO 0
+#endif
+constexpr int kKO = FVC_DX_KO;
 
 template <int IOP>
 __device__ __forceinline__ float in_op_t(float v) {
@@ -131,6 +138,7 @@ __global__ __launch_bounds__(kNT) void conv_dx_kernel(const DxArgs a) {
     bool ok;
   };
   auto fetch = [&](int e, const __amdgpu_buffer_rsrc_t& rx, int iy0, int ix0, Stage& st) {
+    if constexpr ((kKO & 2) != 0) return;
     st.ok = e < tile_items;
     e = st.ok ? e : tile_items - 1;
     const int p = e / C8;
@@ -145,6 +153,7 @@ __global__ __launch_bounds__(kNT) void conv_dx_kernel(const DxArgs a) {
     st.dst = o * psh + p * 8;
   };
   auto store = [&](_Float16* t, const Stage& st) {
+    if constexpr ((kKO & 2) != 0) return;
     float v[8] = {st.v0.x, st.v0.y, st.v0.z, st.v0.w, st.v1.x, st.v1.y, st.v1.z, st.v1.w};
 #pragma unroll
     for (int i = 0; i < 8; ++i) v[i] = in_op_t<IOP>(v[i]);
@@ -231,12 +240,22 @@ __global__ __launch_bounds__(kNT) void conv_dx_kernel(const DxArgs a) {
         const int toffh = __builtin_amdgcn_readlane(tap_tab, t) * 8 + (2 * (q - t * KPT) + lh) * psh;
 #pragma unroll
         for (int m = 0; m < WM; ++m) {
+          if constexpr ((kKO & 4) != 0) {
+            op.ah[m] = h8{} + (_Float16)(q + m + toffh);
+            op.al[m] = h8{} + (_Float16)(q);
+            continue;
+          }
           op.ah[m] = *reinterpret_cast<const h8*>(cur + toffh + pix[m]);
           op.al[m] = *reinterpret_cast<const h8*>(cur + toffh + pix[m] + C8 * psh);
         }
         const uint4* const wk = wcl + ((size_t)q * a.ntp + n0) * kFrag;
 #pragma unroll
         for (int n = 0; n < WN; ++n) {
+          if constexpr ((kKO & 1) != 0) {
+            op.bh[n] = uint4{(unsigned)(q + n), 1u, 2u, 3u};
+            op.bl[n] = uint4{(unsigned)q, 5u, 6u, 7u};
+            continue;
+          }
           op.bh[n] = wk[n * kFrag];
           op.bl[n] = wk[n * kFrag + 64];
         }
@@ -244,6 +263,15 @@ __global__ __launch_bounds__(kNT) void conv_dx_kernel(const DxArgs a) {
       // weights as the A (row) operand, pixels as B: lane (li, lh) ends with 4 consecutive
       // channels of pixel li per register group
       auto mfmas = [&](const Ops& op) {
+        if constexpr ((kKO & 8) != 0) {
+#pragma unroll
+          for (int m = 0; m < WM; ++m)
+#pragma unroll
+            for (int n = 0; n < WN; ++n)
+              acc[m][n][0] += (float)op.ah[m][0] + (float)op.al[m][1] + __builtin_bit_cast(float, op.bh[n].x) +
+                              __builtin_bit_cast(float, op.bl[n].y);
+          return;
+        }
 #pragma unroll
         for (int m = 0; m < WM; ++m)
 #pragma unroll
@@ -352,7 +380,7 @@ __global__ __launch_bounds__(kNT) void conv_dx_kernel(const DxArgs a) {
             float o[4];
 #pragma unroll
             for (int i = 0; i < 4; ++i) o[i] = fmaf(pc[4 * g + i], a.tosc_c, pa[4 * g + i] * a.tosc);
-            const unsigned so = (ok && p0 < a.pcp) ? po + 32u * g : kOob;
+            const unsigned so = (ok && p0 < a.pcp && !(kKO & 16)) ? po + 32u * g : kOob;
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, make_float4(o[0], o[1], o[2], o[3])), ry,
                                                    so, 0, 0);
           }
@@ -394,7 +422,7 @@ __global__ __launch_bounds__(kNT) void conv_dx_kernel(const DxArgs a) {
 #pragma unroll
                 for (int i = 0; i < 4; ++i) v[i] = j0 + i < a.cout ? expf(v[i]) : 0.f;
               }
-              const unsigned so = (ok && j0 < a.coutp) ? vo + 32u * g : kOob;
+              const unsigned so = (ok && j0 < a.coutp && !(kKO & 16)) ? vo + 32u * g : kOob;
               __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, make_float4(v[0], v[1], v[2], v[3])),
                                                      ry, so, 0, 0);
             }
