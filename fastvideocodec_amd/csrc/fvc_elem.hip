@@ -354,6 +354,47 @@ __device__ __forceinline__ float4 up_sample4(const float* src, size_t bbase, int
   return o;
 }
 
+// 64-channel form (Warp_net's c3_u / c4_u, endecoder.py:288-293): 32-bit indexes with the pixel
+// and row divisions as multiply-high by a host-computed ceil(2^32 / d) plus one correction (exact for
+// any 32-bit numerator: the estimate is floor(n / d) or one above it), instead of the generic
+// kernel's 64-bit divisions per float4. Same arithmetic per element as k_up2_add.
+__device__ __forceinline__ unsigned udiv_magic(unsigned n, unsigned d, unsigned m) {
+  unsigned q = __umulhi(n, m);
+  return q * d > n ? q - 1 : q;
+}
+
+__global__ void k_up2_add_q16(const float* __restrict__ src, const float* __restrict__ skip, float* __restrict__ out,
+                              int B, int h, int w, int ac, float scale, unsigned mW, unsigned mH) {
+  const unsigned H = 2u * h, W = 2u * w;
+  const unsigned n = (unsigned)B * H * W * 16u;
+  const float4* s4 = reinterpret_cast<const float4*>(src);
+  for (unsigned e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
+    const unsigned c4 = e & 15u;
+    const unsigned p = e >> 4;
+    const unsigned row = udiv_magic(p, W, mW);
+    const int x = (int)(p - row * W);
+    const unsigned b = udiv_magic(row, H, mH);
+    const int y = (int)(row - b * H);
+    const UpIdx uy = up_index(y, h, (int)H, ac), ux = up_index(x, w, (int)W, ac);
+    const unsigned bb = b * (unsigned)h * (unsigned)w;
+    const float4 a = s4[(bb + (unsigned)uy.i0 * w + ux.i0) * 16u + c4];
+    const float4 bq = s4[(bb + (unsigned)uy.i0 * w + ux.i1) * 16u + c4];
+    const float4 c = s4[(bb + (unsigned)uy.i1 * w + ux.i0) * 16u + c4];
+    const float4 d = s4[(bb + (unsigned)uy.i1 * w + ux.i1) * 16u + c4];
+    float4 v;
+    v.x = (a.x * ux.l0 + bq.x * ux.l1) * uy.l0 + (c.x * ux.l0 + d.x * ux.l1) * uy.l1;
+    v.y = (a.y * ux.l0 + bq.y * ux.l1) * uy.l0 + (c.y * ux.l0 + d.y * ux.l1) * uy.l1;
+    v.z = (a.z * ux.l0 + bq.z * ux.l1) * uy.l0 + (c.z * ux.l0 + d.z * ux.l1) * uy.l1;
+    v.w = (a.w * ux.l0 + bq.w * ux.l1) * uy.l0 + (c.w * ux.l0 + d.w * ux.l1) * uy.l1;
+    if (scale != 1.f) { v.x *= scale; v.y *= scale; v.z *= scale; v.w *= scale; }
+    if (skip) {
+      const float4 sk = reinterpret_cast<const float4*>(skip)[e];
+      v.x = sk.x + v.x; v.y = sk.y + v.y; v.z = sk.z + v.z; v.w = sk.w + v.w;
+    }
+    reinterpret_cast<float4*>(out)[e] = v;
+  }
+}
+
 __global__ void k_up2_add(const float* __restrict__ src, const float* __restrict__ skip, float* __restrict__ out,
                           int B, int h, int w, int cp, int ac, float scale) {
   const int H = 2 * h, W = 2 * w, c4n = cp / 4;
@@ -887,6 +928,11 @@ __global__ __launch_bounds__(kBlk) void k_gc_forward(const float* __restrict__ x
   block_reduce_store<1>(acc, ws);
 }
 
+static int env_flag(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return (v && v[0]) ? atoi(v) : dflt;
+}
+
 static int grid_for(size_t n) {
   size_t g = (n + kBlk - 1) / kBlk;
   if (g > 8192) g = 8192;
@@ -944,8 +990,15 @@ int fvc_upsample2x_add_nhwc(const float* src, const float* skip, float* out, int
                             int align_corners, float scale, fvc_stream_t s) {
   if (!src || !out || cp % 4) return FVC_EINVAL;
   const size_t n = (size_t)batch * 4 * h * w * (cp / 4);
-  hipLaunchKernelGGL(k_up2_add, dim3(grid_for(n)), dim3(kBlk), 0, (hipStream_t)s, src, skip, out, batch, h, w, cp,
-                     align_corners, scale);
+  const unsigned long long H2 = 2ull * h, W2 = 2ull * w;
+  if (cp == 64 && (unsigned long long)batch * H2 * W2 * 16ull < (1ull << 32) && env_flag("FVC_UP2_Q16", 1)) {
+    const unsigned mW = (unsigned)(((1ull << 32) + W2 - 1) / W2), mH = (unsigned)(((1ull << 32) + H2 - 1) / H2);
+    hipLaunchKernelGGL(k_up2_add_q16, dim3(grid_for(n)), dim3(kBlk), 0, (hipStream_t)s, src, skip, out, batch, h, w,
+                       align_corners, scale, mW, mH);
+  } else {
+    hipLaunchKernelGGL(k_up2_add, dim3(grid_for(n)), dim3(kBlk), 0, (hipStream_t)s, src, skip, out, batch, h, w, cp,
+                       align_corners, scale);
+  }
   FVC_CHECK_LAUNCH();
   return 0;
 }
