@@ -126,6 +126,11 @@ struct X3Args {
   float* pool;
   unsigned pool_bytes;
   int toff[4][kMaxTapsX + 1];      // LDS offset (halves) of each tap's window; 0 past ntaps
+  // pair-tap form (stride-1 convs with 16 output channels): an N-tile's rows 16-31 hold the same 16
+  // channels' weights of the odd tap (ky, kx + 1) of each (ky, even kx) pair, multiplied with the even
+  // tap's window: row 16 + c of pixel p is tap (ky, kx + 1)'s product for output pixel p - 1, so the
+  // epilogue adds it from lane p + 1 and every strip of 32 pixels finishes 31 output columns
+  int pt;
 };
 
 typedef float f2v __attribute__((ext_vector_type(2)));
@@ -250,7 +255,8 @@ __global__ __launch_bounds__(NWV * 64) void conv_x3_kernel(const X3Args a) {
   const int li = lane & 31;
   const int lh = lane >> 5;
   const int b = blockIdx.z;
-  const int tiles_x = (a.Wq + TW - 1) / TW;
+  const int TWo = a.pt ? TW - 1 : TW;  // output columns per tile
+  const int tiles_x = (a.Wq + TWo - 1) / TWo;
   const int ntiles = tiles_x * ((a.Hq + TH - 1) / TH);
   // persistent over a contiguous run of work items w = tile * nclass + class (row-major tiles:
   // neighbours share halo rows and columns in this CU's L2; all parity classes of a transposed
@@ -329,7 +335,7 @@ __global__ __launch_bounds__(NWV * 64) void conv_x3_kernel(const X3Args a) {
     const int c = p - r * a.ic;
     if constexpr ((kKO & 32) != 0) { tile = 0; ch = 0; }
     const int iy = (tile / tiles_x) * TH * a.sin + a.dymin + r;
-    const int ix = (tile % tiles_x) * TW * a.sin + a.dxmin + c;
+    const int ix = (tile % tiles_x) * TWo * a.sin + a.dxmin + c;
     const bool inb = (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
     const unsigned off = inb ? ((unsigned)(iy * a.W + ix) * (unsigned)a.cinp + (unsigned)(ch * CC + o * 8)) * 4u : kOob;
     st.v0 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rx, off, 0, 0));
@@ -610,8 +616,8 @@ __global__ __launch_bounds__(NWV * 64) void conv_x3_kernel(const X3Args a) {
     // Activation as one max: relu = max(v, 0*v), lrelu = max(v, 0.1*v), none = max(v, 1*v).
     // Pad channels need no select: their weights and bias are 0 and every residual tensor's pad
     // channels are 0, so they come out 0 -- except after exp (POST), which selects them to 0.
-    const int qy0 = (tile / tiles_x) * TH, qx0 = (tile % tiles_x) * TW;
-    const bool px_ok = qx0 + li < a.Wq;
+    const int qy0 = (tile / tiles_x) * TH, qx0 = (tile % tiles_x) * TWo;
+    const bool px_ok = qx0 + li < a.Wq && li < TWo;
     auto pix_of = [&](int m) {  // output pixel index of this lane in strip m
       const unsigned qy = qy0 + wm_ * WM + m;
       return ((unsigned)b * a.Ho + qy * a.sout + a.oy0[cls]) * a.Wo + a.ox0[cls] + (unsigned)(qx0 + li) * a.sout;
@@ -713,6 +719,17 @@ __global__ __launch_bounds__(NWV * 64) void conv_x3_kernel(const X3Args a) {
         if (!kResPipe) load_res(t, rv[t & 1]);
         else if (t + 1 < NTL) load_res(t + 1, rv[(t + 1) & 1]);
       }
+      // pair-tap form: the odd taps' products of this lane's output pixel sit in rows 16-31
+      // (register groups 2, 3) of the next lane
+      float sh[8];
+      if (a.pt) {
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          const float bv = kAcc1 ? acc[m][n][8 + r] * a.osc
+                                 : fmaf(cor[kAcc1 ? 0 : m][kAcc1 ? 0 : n][8 + r], a.osc_c, acc[m][n][8 + r] * a.osc);
+          sh[r] = __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(((lane + 1) & 63) * 4, __builtin_bit_cast(int, bv)));
+        }
+      }
       const unsigned vo = voff_of(m, n);
       const bool row_ok = qy0 + wm_ * WM + m < a.Hq && px_ok;
 #pragma unroll
@@ -725,8 +742,9 @@ __global__ __launch_bounds__(NWV * 64) void conv_x3_kernel(const X3Args a) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int r = 4 * g + i;
-          const float tv = kAcc1 ? fmaf(acc[m][n][r], a.osc, bb[i])
-                                 : fmaf(cor[kAcc1 ? 0 : m][kAcc1 ? 0 : n][r], a.osc_c, fmaf(acc[m][n][r], a.osc, bb[i]));
+          float tv = kAcc1 ? fmaf(acc[m][n][r], a.osc, bb[i])
+                           : fmaf(cor[kAcc1 ? 0 : m][kAcc1 ? 0 : n][r], a.osc_c, fmaf(acc[m][n][r], a.osc, bb[i]));
+          if (a.pt && g < 2) tv += sh[r];
           v[i] = fmaxf(tv, tv * a.act_slope);
         }
         if (a.res) {
@@ -798,6 +816,7 @@ __global__ __launch_bounds__(NWV * 64) void conv_x3_kernel(const X3Args a) {
 // ------------------------------------------------------------------ host-side geometry
 struct X3Cfg {
   int cinp, coutp, ntp, cc, wm, wn, nw, nclass, nchunks, th, sin, sout;
+  int pt;     // pair-tap form (16 output channels, stride 1): (ky, even kx) pairs, see X3Args::pt
   int dx;     // stride-2 transposed conv on fvc_deconv_x3.hip (all classes per staged tile, one chunk)
   int wl;     // weights staged in LDS by LDS-DMA (FVC_X3_WL; chosen at pack time: it can shrink cc)
   int wnmax;  // N-tiles per block the LDS weight buffers are sized for
@@ -841,13 +860,14 @@ static bool x3_cfg(int cin, int cout, int ks, int stride, int transposed, X3Cfg&
   c.ntp = fvc_cdiv(c.coutp, 32);
   if (c.ntp > 4) return false;
   const int pad = ks / 2;
+  c.pt = (!transposed && stride == 1 && c.coutp == 16 && ks >= 3 && env_int("FVC_X3_PT", 1)) ? 1 : 0;
   if (!transposed) {
     c.nclass = 1;
     c.sin = stride;
     c.sout = 1;
     c.ntaps[0] = 0;
     for (int ky = 0; ky < ks; ++ky)
-      for (int kx = 0; kx < ks; ++kx) {
+      for (int kx = 0; kx < ks; kx += c.pt ? 2 : 1) {
         const int t = c.ntaps[0]++;
         c.tky[0][t] = ky; c.tkx[0][t] = kx;
         c.tdy[0][t] = ky - pad; c.tdx[0][t] = kx - pad;
@@ -1260,6 +1280,8 @@ static int run_x3(const float* x, const void* wpack, float osc, const float* bia
   a.xcd = env_int("FVC_X3_XCD", 1) ? 1 : 0;
   a.prio = env_int("FVC_X3_PRIO", 0) ? 1 : 0;
   a.ic = 31 * c.sin + 1 + (c.dxmax - c.dxmin);
+  a.pt = c.pt;
+  if (c.pt && (tw || pool)) return FVC_EINVAL;
   a.half = c.sin == 2 ? (a.ic + 1) / 2 : 0;
   a.inv_ic = 1.0f / (float)a.ic;
   a.act_slope = act == FVC_ACT_RELU ? 0.f : (act == FVC_ACT_LRELU ? 0.1f : 1.f);
@@ -1402,14 +1424,17 @@ int fvc_conv_x3_pack_weight(const float* w, void* wp, float* osc_out, int cin, i
             const int kb = 2 * q + lh;
             const int t = kb / c8n, o = kb % c8n;
             const int j = nt * 32 + li;
-            if (t >= c.ntaps[cl] || j >= cout) continue;
-            const int ky = c.tky[cl][t], kx = c.tkx[cl][t];
+            if (t >= c.ntaps[cl] || (!c.pt && j >= cout)) continue;
+            const int ky = c.tky[cl][t];
+            const int kx = c.tkx[cl][t] + (c.pt && li >= 16 ? 1 : 0);  // pair-tap: rows 16-31 = odd tap
+            const int jo = c.pt ? (li & 15) : j;                          // output channel of row li
+            if (kx >= ks || jo >= cout) continue;
             const size_t frag = ((((size_t)c.wcls[cl] + (((size_t)ch * c.nks[cl] + q) * c.ntp + nt) * kFrag)) + lane) * 8;
             for (int e = 0; e < 8; ++e) {
               const int ci = ch * c.cc + o * 8 + e;
               if (ci >= cin) continue;
-              const float v = (transposed ? w[(((size_t)ci * cout + j) * ks + ky) * ks + kx]
-                                          : w[(((size_t)j * cin + ci) * ks + ky) * ks + kx]) * sc;
+              const float v = (transposed ? w[(((size_t)ci * cout + jo) * ks + ky) * ks + kx]
+                                          : w[(((size_t)jo * cin + ci) * ks + ky) * ks + kx]) * sc;
               const _Float16 hi = (_Float16)v;
               out[frag + e] = hi;  // plane 0 (hi): lanes 0..63
               if (kAcc1) {
@@ -1457,7 +1482,7 @@ int fvc_x3_tap_pack_weight(const float* w, void* wp, float* osc_out, int np, int
 
 int fvc_conv_x3_tap_supported(int cin, int cout, int ksize, int stride, int transposed, int pcp) {
   X3Cfg c;
-  if (!x3_cfg(cin, cout, ksize, stride, transposed, c) || c.wl || pcp <= 0 || pcp > 32 || (pcp & 3)) return 0;
+  if (!x3_cfg(cin, cout, ksize, stride, transposed, c) || c.wl || c.pt || pcp <= 0 || pcp > 32 || (pcp & 3)) return 0;
   if (c.dx) return c.ntp == 4;  // the all-classes kernel's tap form: 1 strip x 4 N-tiles
   const int wm = c.ntp == 4 ? 1 : c.wm;
   return (wm == 2 && c.ntp <= 2) || (wm == 1 && c.ntp == 4);
@@ -1487,7 +1512,7 @@ int fvc_deconv2d_nhwc_x3_tap(const float* x, const void* wpack, float osc, const
 
 int fvc_conv_x3_pool_supported(int cin, int cout, int ksize) {
   X3Cfg c;
-  return x3_cfg(cin, cout, ksize, 1, 0, c) && !c.wl && c.wm == 2 && c.ntp <= 2;
+  return x3_cfg(cin, cout, ksize, 1, 0, c) && !c.wl && !c.pt && c.wm == 2 && c.ntp <= 2;
 }
 
 int fvc_conv2d_nhwc_x3_pool(const float* x, const void* wpack, float osc, const float* bias, const float* res,

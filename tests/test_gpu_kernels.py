@@ -540,3 +540,30 @@ def test_rans_decode_tails_and_escapes(dev):
     idx = rng.integers(0, 64, (S, n)).astype(np.int32)
     enc = lc.encode(torch.from_numpy(sym).to(dev), torch.from_numpy(idx).to(dev))
     assert (lc.decode(enc, torch.from_numpy(idx).to(dev)).cpu().numpy() == sym).all()
+
+
+@pytest.mark.parametrize("shape", [(2, 32, 16, 7, 20, 67), (1, 16, 16, 3, 13, 31), (3, 32, 16, 5, 9, 95)])
+def test_conv_pair_tap_form(dev, shape, monkeypatch):
+    """16-output-channel convs in pair-tap form (SpyNet conv4, endecoder.py:155: rows 16-31 of the
+    MFMA tile carry the odd tap of each (ky, even kx) pair, added from the next lane; 31 output columns
+    per 32-pixel strip) against float64 torch and against the plain padded-N form (FVC_X3_PT=0);
+    widths cut at every strip edge."""
+    B, cin, cout, k, H, W = shape
+    g = torch.Generator().manual_seed(cin + k + W)
+    x = torch.randn(B, cin, H, W, generator=g)
+    w = torch.randn(cout, cin, k, k, generator=g) * (1.0 / (cin * k * k) ** 0.5)
+    b = torch.randn(cout, generator=g) * 0.1
+    ref = F.relu(F.conv2d(x.double(), w.double(), b.double(), 1, k // 2))
+    xd = to_nhwc(x).to(dev)
+    outs = {}
+    for pt in ("1", "0"):
+        monkeypatch.setenv("FVC_X3_PT", pt)
+        pc = K.PackedConv(w, b, k, 1, False, dev, precision="x3")
+        assert pc.x3
+        outs[pt] = pc(xd, act=K.ACT_RELU)
+    torch.cuda.synchronize()
+    scale = float(ref.abs().max())
+    e1 = float((from_nhwc(outs["1"].cpu(), cout).double() - ref).abs().max())
+    e0 = float((from_nhwc(outs["0"].cpu(), cout).double() - ref).abs().max())
+    print(f"{shape}: pair-tap err {e1 / scale:.2e}, padded-N err {e0 / scale:.2e} (of output scale)")
+    assert e1 <= 2e-6 * scale, (e1, e0, scale)
