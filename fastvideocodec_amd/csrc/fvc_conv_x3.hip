@@ -339,7 +339,9 @@ __global__ __launch_bounds__(NWV * 64) void conv_x3_kernel(const X3Args a) {
     const bool inb = (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
     const unsigned off = inb ? ((unsigned)(iy * a.W + ix) * (unsigned)a.cinp + (unsigned)(ch * CC + o * 8)) * 4u : kOob;
     st.v0 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rx, off, 0, 0));
-    st.v1 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rx, off + 16u, 0, 0));
+    // 4-channel inputs (cin 2 / 3): the octet's upper half is zero padding -- the second load goes past
+    // the descriptor's range and returns zeros (no branch)
+    st.v1 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rx, a.cinp == 4 ? kOob : off + 16u, 0, 0));
     const int cpos = hf ? ((c & 1) * hf + (c >> 1)) : c;
     st.dst = o * a.ps + (r * a.ic + cpos) * 8;  // plane o (hi), pixel-minor
   };
@@ -849,7 +851,10 @@ static bool x3_cfg(int cin, int cout, int ks, int stride, int transposed, X3Cfg&
     return false;
   c.cinp = fvc_rup(cin, 4);
   c.coutp = fvc_rup(cout, 4);
-  if (c.cinp % 8) return false;
+  // cin padded to 4 (cin 2 / 3: mvEncoder conv1, resEncoder conv1) runs as one zero-extended octet:
+  // the staging loads 4 channels per pixel and pads the other 4 with zeros, so no widened copy of
+  // the input is needed (FVC_X3_CIN4=0 keeps these layers on the fp32 kernels)
+  if (c.cinp % 8 && !(c.cinp == 4 && env_int("FVC_X3_CIN4", 1))) return false;
   // cout <= 4 (N padded to one 32-wide tile): measured faster than the VALU small-N kernel for the
   // 3x3 / 5x5 layers (Warp_net conv6, mvDecoder conv8, resDecoder deconv4), slower for SpyNet's
   // 7x7 16->2 (scripts/conv_micro.py); FVC_X3_SMALLN=0/1 forces either way
@@ -969,7 +974,7 @@ static bool x3_cfg(int cin, int cout, int ks, int stride, int transposed, X3Cfg&
     else if (c.wm > 1) c.wm /= 2;
     else return false;
   }
-  c.nchunks = c.cinp / c.cc;
+  c.nchunks = c.cinp == 4 ? 1 : c.cinp / c.cc;
   c.wn = 1;
   long long off = 0;
   for (int cl = 0; cl < c.nclass; ++cl) {

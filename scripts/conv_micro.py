@@ -27,6 +27,8 @@ CASES = {
     "c3_128_eighth": (128, 128, 3, 1, False, 136, 240),
     "c7_8_32_full": (8, 32, 7, 1, False, 1088, 1920),
     "c3_6_64_full": (6, 64, 3, 1, False, 1088, 1920),
+    "c3s2_2_128_full": (2, 128, 3, 2, False, 1088, 1920),   # mvEncoder conv1
+    "c5s2_3_64_full": (3, 64, 5, 2, False, 1088, 1920),     # resEncoder conv1
     "c3s2_128_half": (128, 128, 3, 2, False, 544, 960),
     "c3_64_3_full": (64, 3, 3, 1, False, 1088, 1920),
     "d5_64_3_half": (64, 3, 5, 2, True, 1088, 1920),

@@ -145,7 +145,8 @@ def test_x3_tap_pack_layout(np_cin):
 
 def test_x3_rejects_unsupported_layers():
     lib = _lib.load()
-    assert lib.fvc_conv_x3_supported(2, 128, 3, 2, 0) == 0  # cin padded to 4: fp32 kernel
+    assert lib.fvc_conv_x3_supported(2, 128, 3, 2, 0) == 1  # cin padded to 4: one zero-extended octet
+    assert lib.fvc_conv_x3_supported(3, 64, 5, 2, 0) == 1   # resEncoder conv1
     assert lib.fvc_conv_x3_supported(16, 2, 7, 1, 0) == 0   # 7x7 cout <= 4: VALU small-N kernel
     assert lib.fvc_conv_x3_wpack_bytes(16, 2, 7, 1, 0) == 0
     assert lib.fvc_conv_x3_supported(64, 3, 3, 1, 0) == 1   # 3x3 cout <= 4: N padded to one MFMA tile
