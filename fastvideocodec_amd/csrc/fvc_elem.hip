@@ -656,6 +656,212 @@ __global__ __launch_bounds__(64 * kGdnWaves) void k_gdn_tap_mfma(const float* __
   if (!(mx < 65000.f) && ovf) atomicOr(ovf, 1);
 }
 
+// GDN / IGDN with the norm on the split-precision fp16 matrix cores (the conv kernels' scheme):
+// norm = beta + gamma . x^2 is a [64 out ch] x [64 in ch] x [32 px] GEMM per 32-pixel group with
+// gamma as the row operand (one launch-wide scale 2^kw: max |gamma| * 2^kw in [2^13, 2^14)) and
+// x^2 * 2^-8 as the column operand, both split exactly into fp16 hi + lo * 2^-11:
+// 2 N-tiles x 4 k-blocks x 3 v_mfma_f32_32x32x16_f16 (24 MFMAs of 8 passes) instead of 64
+// v_mfma_f32_32x32x2_f32 of 16 passes -- the fp32 form's matrix time is as long as its HBM time.
+// Lane (li, lh) owns pixel li and channels 32t + 8g + 4lh + {0..3} (t = 0..1, g = 0..3) from load
+// to store: k-block kb = 2t + gp orders its channels {16gp + 4lh + 0-3 | 16gp + 8 + 4lh + 0-3}
+// (+32t), so a lane's column operand is its own x / accumulator registers 8gp .. 8gp + 7 and no
+// LDS tile is needed (the same order as fvc_x3_tap_pack_weight: in the tap form (NPT > 0) the
+// normalised y already is the B fragment of the tap GEMM). The omitted lo * lo term and the lo
+// roundings are ~2^-22 relative per product; every term of the norm is >= 0, so the norm carries
+// that relative error (fp32 chain: ~2^-24 per add). A group with a value x^2 * 2^-8 >= 65000
+// (|x| >= 4079), inf or NaN runs the fp32 MFMA chain instead (wave-uniform branch, gamma read
+// from L2): results never depend on the fp16 range.
+template <int NPT, bool INV>
+__global__ __launch_bounds__(256, 2) void k_gdn_x3(const float* __restrict__ x, float* __restrict__ out,
+                                                   const float* __restrict__ beta, const float* __restrict__ gamma,
+                                                   const uint4* __restrict__ tw, float4 tosc, size_t npix,
+                                                   int pcp, int* ovf) {
+  __shared__ float4 sbeta[16];
+  __shared__ uint4 sg[2 * 4 * 2 * 64];  // row-operand fragments [n][kb][hi, lo][lane]
+  __shared__ uint4 stw[NPT > 0 ? NPT * 512 : 1];  // the tap pack (fvc_x3_tap_pack_weight layout)
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int li = lane & 31, lh = lane >> 5;
+  if (threadIdx.x < 64) reinterpret_cast<float*>(sbeta)[threadIdx.x] = beta[threadIdx.x];
+  if constexpr (NPT > 0)
+    for (int i = threadIdx.x; i < NPT * 512; i += 256) stw[i] = tw[i];
+  // row operand: lane (li, lh) -> out channel 32n + li, k-block kb's 8 channels of half lh; every
+  // wave reads all 4096 entries (the same scale in every wave of the launch), wave 0 stores them
+  float gv[2][4][8];
+  float gmax = 0.f;
+#pragma unroll
+  for (int n = 0; n < 2; ++n)
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int ch = 32 * (kb >> 1) + 16 * (kb & 1) + 4 * lh + (e < 4 ? e : 4 + e);
+        gv[n][kb][e] = gamma[(32 * n + li) * 64 + ch];
+        gmax = fmaxf(gmax, fabsf(gv[n][kb][e]));
+      }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) gmax = fmaxf(gmax, __shfl_xor(gmax, o, 64));
+  int ge = 0;
+  (void)frexpf(gmax, &ge);
+  const int kw = gmax > 0.f ? 14 - ge : 0;
+  if (wave == 0) {
+#pragma unroll
+    for (int n = 0; n < 2; ++n)
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb) {
+        gh8 h8, l8;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float s = ldexpf(gv[n][kb][e], kw);
+          const _Float16 h = (_Float16)s;
+          h8[e] = h;
+          l8[e] = (_Float16)((s - (float)h) * 2048.f);
+        }
+        sg[((n * 4 + kb) * 2) * 64 + lane] = __builtin_bit_cast(uint4, h8);
+        sg[((n * 4 + kb) * 2 + 1) * 64 + lane] = __builtin_bit_cast(uint4, l8);
+      }
+  }
+  const float sc = ldexpf(1.f, 8 - kw), scc = ldexpf(1.f, 8 - kw - 11);
+  const float ts[4] = {tosc.x, tosc.y, tosc.z, tosc.w};
+  __syncthreads();
+  const size_t ngroups = (npix + 31) / 32;
+  float4 nx[8];  // nx[2 kb + h]: channels 32t + 16gp + 8h + 4lh + 0..3
+  auto fetch = [&](size_t gi) {
+    const size_t p = gi * 32 + li;
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      nx[k] = p < npix ? *reinterpret_cast<const float4*>(x + p * 64 + 16 * (k >> 1) + 8 * (k & 1) + 4 * lh)
+                       : make_float4(0.f, 0.f, 0.f, 0.f);
+  };
+  const size_t gstep = (size_t)gridDim.x * 4;
+  size_t gi = (size_t)blockIdx.x * 4 + wave;
+  float mx = 0.f;
+  if (gi < ngroups) fetch(gi);
+  for (; gi < ngroups; gi += gstep) {
+    // keeps the loop-invariant fragment reads from LDS inside the loop (hoisted, they would take
+    // 64 registers and spill)
+    asm volatile("" ::: "memory");
+    const size_t p = gi * 32 + li;
+    // xr[t][r]: channel 32t + 8(r / 4) + 4lh + r % 4 (the accumulator layout)
+    float xr[2][16];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int t = k >> 2, r0 = 4 * (k & 3);
+      xr[t][r0] = nx[k].x; xr[t][r0 + 1] = nx[k].y; xr[t][r0 + 2] = nx[k].z; xr[t][r0 + 3] = nx[k].w;
+    }
+    if (gi + gstep < ngroups) fetch(gi + gstep);
+    gh8 sh[4], sl[4];
+    bool big = false;
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float v = xr[kb >> 1][8 * (kb & 1) + e];
+        const float s = (v * v) * 0.00390625f;
+        big |= !(s < 65000.f);
+        const _Float16 h = (_Float16)s;
+        sh[kb][e] = h;
+        sl[kb][e] = (_Float16)((s - (float)h) * 2048.f);
+      }
+    // per N-tile: norm (x3 MFMAs, or the fp32 chain for a group out of fp16 range), then
+    // y = x / sqrt(norm) (GDN) or x * sqrt(norm) (IGDN), norm = sum + beta, written over x (tile 0's
+    // y is parked until tile 1's fp32 chain has read x)
+    const bool slow = __any(big);
+    float y0[16];
+    const float s1 = slow ? 1.f : sc, s2 = slow ? 0.f : scc;
+#pragma unroll
+    for (int n = 0; n < 2; ++n) {
+      f32x16 a, c;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) a[r] = c[r] = 0.f;
+      if (!slow) {
+#pragma unroll
+        for (int kb = 0; kb < 4; ++kb) {
+          const gh8 wh = __builtin_bit_cast(gh8, sg[((n * 4 + kb) * 2) * 64 + lane]);
+          const gh8 wl = __builtin_bit_cast(gh8, sg[((n * 4 + kb) * 2 + 1) * 64 + lane]);
+          a = __builtin_amdgcn_mfma_f32_32x32x16_f16(wh, sh[kb], a, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_f16(wl, sh[kb], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_f16(wh, sl[kb], c, 0, 0, 0);
+        }
+      } else {
+        // v_mfma_f32_32x32x2_f32, k = (register s of the lane, half lh)
+#pragma unroll
+        for (int s = 0; s < 32; ++s) {
+          const int t = s >> 4, r = s & 15;
+          const int ch = 32 * t + 8 * (r >> 2) + 4 * lh + (r & 3);
+          const float v = xr[t][r];
+          a = __builtin_amdgcn_mfma_f32_32x32x2f32(gamma[(32 * n + li) * 64 + ch], v * v, a, 0, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const float4 b = sbeta[8 * n + 2 * g + lh];
+        const float bb[4] = {b.x, b.y, b.z, b.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float nv = sqrtf(fmaf(c[4 * g + i], s2, a[4 * g + i] * s1) + bb[i]);
+          const float xv = xr[n][4 * g + i];
+          const float yv = INV ? xv * nv : xv / nv;
+          if (n == 0) y0[4 * g + i] = yv;
+          else xr[1][4 * g + i] = yv;
+        }
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) xr[0][r] = y0[r];
+    float (&yr)[2][16] = xr;
+    if constexpr (NPT == 0) {
+      if (p < npix) {
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int g = 0; g < 4; ++g)
+            *reinterpret_cast<float4*>(out + p * 64 + 32 * t + 8 * g + 4 * lh) =
+                make_float4(yr[t][4 * g], yr[t][4 * g + 1], yr[t][4 * g + 2], yr[t][4 * g + 3]);
+      }
+    } else {
+      // the tap GEMM: y registers 8gp .. 8gp + 7 of tile t are the k16 block kb = 2t + gp
+      const bool px_ok = p < npix;
+      gh8 yh[4], yl[4];
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float f = px_ok ? yr[kb >> 1][8 * (kb & 1) + e] : 0.f;
+          const _Float16 h = (_Float16)f;
+          yh[kb][e] = h;
+          yl[kb][e] = (_Float16)((f - (float)h) * 2048.f);
+          mx = fmaxf(mx, fabsf(f));
+        }
+#pragma unroll
+      for (int pt = 0; pt < NPT; ++pt) {
+        f32x16 pa, pc;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) pa[r] = pc[r] = 0.f;
+#pragma unroll
+        for (int kb = 0; kb < 4; ++kb) {
+          const uint4* f = stw + ((pt * 4 + kb) * 2) * 64 + lane;
+          const gh8 wh = __builtin_bit_cast(gh8, f[0]), wl = __builtin_bit_cast(gh8, f[64]);
+          pa = __builtin_amdgcn_mfma_f32_32x32x16_f16(wh, yh[kb], pa, 0, 0, 0);
+          pc = __builtin_amdgcn_mfma_f32_32x32x16_f16(wl, yh[kb], pc, 0, 0, 0);
+          pc = __builtin_amdgcn_mfma_f32_32x32x16_f16(wh, yl[kb], pc, 0, 0, 0);
+        }
+        const float s1 = ts[pt], s2 = ts[pt] * (1.0f / 2048.f);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int pp = pt * 32 + 8 * g + 4 * lh;
+          if (px_ok && pp < pcp) {
+            float o[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) o[i] = fmaf(pc[4 * g + i], s2, pa[4 * g + i] * s1);
+            *reinterpret_cast<float4*>(out + p * pcp + pp) = make_float4(o[0], o[1], o[2], o[3]);
+          }
+        }
+      }
+    }
+  }
+  if (NPT > 0 && !(mx < 65000.f) && ovf) atomicOr(ovf, 1);
+}
+
 // ------------------------------------------------------------------ deterministic reductions
 template <int K>
 __device__ void block_reduce_store(double (&v)[K], double* out) {
@@ -1155,10 +1361,29 @@ int fvc_gc_forward(const float* x, const float* scale, const float* mu, float* x
   return 0;
 }
 
+// persistent grid of the split-precision GDN kernels: 4 groups of 32 pixels per block and pass
+static unsigned gdn_x3_blocks(size_t npix) {
+  static const int cap = env_flag("FVC_GDN_BLOCKS", 1024);
+  size_t nb = ((npix + 31) / 32 + 3) / 4;
+  if (nb > (size_t)cap) nb = (size_t)cap;
+  return nb < 1 ? 1u : (unsigned)nb;
+}
+
 int fvc_gdn_nhwc(const float* x, float* y, const float* beta, const float* gamma, int batch, int h, int w, int c,
                  int inverse, fvc_stream_t s) {
   if (!x || !y || !beta || !gamma || c != 64) return FVC_EINVAL;
   const size_t npix = (size_t)batch * h * w;
+  if (env_flag("FVC_GDN_X3", 1)) {
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (inverse)
+      hipLaunchKernelGGL((k_gdn_x3<0, true>), dim3(gdn_x3_blocks(npix)), dim3(256), 0, (hipStream_t)s, x, y, beta, gamma,
+                         (const uint4*)nullptr, z4, npix, 0, (int*)nullptr);
+    else
+      hipLaunchKernelGGL((k_gdn_x3<0, false>), dim3(gdn_x3_blocks(npix)), dim3(256), 0, (hipStream_t)s, x, y, beta,
+                         gamma, (const uint4*)nullptr, z4, npix, 0, (int*)nullptr);
+    FVC_CHECK_LAUNCH();
+    return 0;
+  }
   size_t nblk = ((npix + 31) / 32 + kGdnWaves - 1) / kGdnWaves;
   if (nblk > 2048) nblk = 2048;
   if (nblk < 1) nblk = 1;
@@ -1182,6 +1407,18 @@ int fvc_gdn_tap_nhwc(const float* x, float* P, const float* beta, const float* g
   for (int i = 0; i < ntiles; ++i) t[i] = tap_osc[i];
   const float4 tosc = make_float4(t[0], t[1], t[2], t[3]);
   const uint4* tw = (const uint4*)tap_wpack;
+  if (env_flag("FVC_GDN_X3", 1)) {
+    const unsigned nb = gdn_x3_blocks(npix);
+#define FVC_GX(N, I)                                                                                           \
+  if (ntiles == N && !!inverse == I)                                                                           \
+    hipLaunchKernelGGL((k_gdn_x3<N, I>), dim3(nb), dim3(256), 0, (hipStream_t)s, x, P, beta, gamma, tw, tosc, npix, \
+                       pcp, overflow_flag);
+    FVC_GX(1, false) FVC_GX(2, false) FVC_GX(3, false) FVC_GX(4, false)
+    FVC_GX(1, true) FVC_GX(2, true) FVC_GX(3, true) FVC_GX(4, true)
+#undef FVC_GX
+    FVC_CHECK_LAUNCH();
+    return 0;
+  }
 #define FVC_GT(N)                                                                                               \
   if (ntiles == N) {                                                                                          \
     hipLaunchKernelGGL(k_gdn_tap_mfma<N>, dim3((unsigned)nblk), dim3(64 * kGdnWaves), 0, (hipStream_t)s, x, P, beta, \

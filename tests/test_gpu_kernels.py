@@ -431,6 +431,61 @@ def test_gdn(dev, seeded_sd, inverse):
     close(from_nhwc(y.cpu(), 64), ref, 2e-6)
 
 
+@pytest.mark.parametrize("inverse", [False, True])
+@pytest.mark.parametrize("shape", [(1, 12, 20), (2, 13, 22), (3, 1, 31), (1, 37, 65)])
+def test_gdn_x3_vs_fp32_and_float64(dev, shape, inverse, monkeypatch):
+    """The split-precision GDN kernel (k_gdn_x3: norm on fp16 hi/lo MFMAs) against float64 torch
+    (GDN.py:63-93) and against the fp32-MFMA kernel (FVC_GDN_X3=0) at ragged pixel counts (groups
+    of 32 cut anywhere), with off-diagonal gamma entries 6 orders of magnitude below the diagonal;
+    a 5000-valued input sends its group down the fp32 chain inside the kernel with no flag."""
+    B, H, W = shape
+    g = torch.Generator().manual_seed(H * W + int(inverse))
+    x = torch.randn(B, 64, H, W, generator=g) * 3
+    beta = torch.rand(64, generator=g) + 0.5
+    gamma = torch.rand(64, 64, generator=g) * 1e-7 + torch.eye(64) * 0.1
+    gamma[5, :] = torch.rand(64, generator=g) * 0.02
+    big = x.clone()
+    big.view(-1)[(B * 64 * H * W) // 2] = 5000.0
+    for xin in (x, big):
+        norm = torch.sqrt(F.conv2d(xin.double() ** 2, gamma.double()[:, :, None, None], beta.double()))
+        ref = xin.double() * norm if inverse else xin.double() / norm
+        outs = {}
+        for flag in ("1", "0"):
+            monkeypatch.setenv("FVC_GDN_X3", flag)
+            outs[flag] = from_nhwc(K.gdn(to_nhwc(xin).to(dev), beta.to(dev), gamma.to(dev).contiguous(),
+                                         inverse).cpu(), 64).double()
+        scale = float(ref.abs().max())
+        e3 = float((outs["1"] - ref).abs().max())
+        e32 = float((outs["0"] - ref).abs().max())
+        print(f"{shape} inv={inverse} big={xin is big}: x3 {e3 / scale:.2e}, fp32 {e32 / scale:.2e} of scale")
+        assert e3 <= 1e-6 * scale and e3 <= 4 * e32 + 1e-7 * scale, (e3, e32, scale)
+
+
+def test_gdn_x3_tap_form_vs_fp32_form(dev, monkeypatch):
+    """GDN + the next layer's tap partials: the x3 kernel against the fp32-MFMA kernel and float64."""
+    g = torch.Generator().manual_seed(77)
+    B, H, W = 2, 17, 29
+    x = torch.randn(B, 64, H, W, generator=g)
+    beta = torch.rand(64, generator=g) + 0.5
+    gamma = torch.rand(64, 64, generator=g) * 0.05 + torch.eye(64) * 0.2
+    w = torch.randn(64, 3, 5, 5, generator=g) * (1.0 / (64 * 25) ** 0.5)
+    b = torch.randn(3, generator=g) * 0.1
+    norm = torch.sqrt(F.conv2d(x.double() ** 2, gamma.double()[:, :, None, None], beta.double()))
+    ref = F.conv_transpose2d(x.double() * norm, w.double(), b.double(), 2, 2, 1)
+    t = K.GdnTap(w, b, 5, 2, True, dev)
+    outs = {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("FVC_GDN_X3", flag)
+        K.x3_overflow(reset=True)
+        outs[flag] = from_nhwc(t(to_nhwc(x).to(dev), beta.to(dev), gamma.to(dev).contiguous(), True).cpu(), 3)
+        torch.cuda.synchronize()
+        assert not K.x3_overflow(reset=True)
+    scale = float(ref.abs().max())
+    e3 = float((outs["1"].double() - ref).abs().max())
+    e32 = float((outs["0"].double() - ref).abs().max())
+    assert e3 <= 2e-6 * scale and e3 <= 3 * e32 + 1e-7 * scale, (e3, e32, scale)
+
+
 def test_bits(dev, seeded_sd):
     g = torch.Generator().manual_seed(5)
     feat = torch.randn(1, 96, 8, 12, generator=g) * 4
