@@ -70,6 +70,8 @@ constexpr unsigned kOob = 0xFFFFFF00u;
 constexpr int kRsrcFlags = 0x00020000;
 constexpr int kPostPool = 1;
 constexpr int kPostTap = 2;
+constexpr int kResPost = 1;
+constexpr int kResPre = 2;
 
 
 struct WinoArgs {
@@ -90,6 +92,9 @@ struct WinoArgs {
   const uint4* tw;
   float tosc, tosc_c;    // 2^-kt, 2^-kt-11
   int pcp;
+  // pixel pitch (floats) of x and of y / res: 64, or 128 for a quarter of a 128 -> 128 conv
+  // (x, y, res then point at the first channel of their 64-channel half)
+  int xp, yp;
 };
 
 typedef __attribute__((address_space(3))) void* lds_ptr;
@@ -200,7 +205,9 @@ __device__ __forceinline__ void split2(float v0, float v1, unsigned& hi, unsigne
       : "v"(r0), "v"(r1), "s"(kLoScale));
 }
 
-template <int IOP, int POST, bool RES, int ACT>
+// RES: 0 none, kResPost = y = act(conv + bias) + res (ResBlock), kResPre = y = act(conv + bias + res)
+// (the second input half of a 128 -> 128 conv adding the first half's partial sum)
+template <int IOP, int POST, int RES, int ACT>
 __global__ __launch_bounds__(256, 1) void conv_wino_kernel(const WinoArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* const sbias = reinterpret_cast<float*>(smem);
@@ -229,7 +236,7 @@ __global__ __launch_bounds__(256, 1) void conv_wino_kernel(const WinoArgs a) {
           for (int pl = 0; pl < 2; ++pl)
             u[q][n][kk][pl] = __builtin_bit_cast(h8, src[(((q * 4 + n) * 2 + kk) * 2 + pl) * 64]);
   }
-  if (tid < kC) sbias[tid] = a.bias[tid];
+  if (tid < kC) sbias[tid] = a.bias ? a.bias[tid] : 0.f;
 
   // rows of the 4x4 patch this wave's transform row combines: E = d[ra] + sb * d[rb]
   // (B^T rows (1,0,-1,0) (0,1,1,0) (0,-1,1,0) (0,1,0,-1)), then V[r][.] = E B (x-transform)
@@ -254,15 +261,16 @@ __global__ __launch_bounds__(256, 1) void conv_wino_kernel(const WinoArgs a) {
 #pragma unroll
     for (int m = 0; m < 3; ++m) {
       const int ix = 32 * g - 1 + dma_lc[m];
-      vo[m] = (unsigned)ix < (unsigned)W ? (unsigned)(ix * kC + dma_ch[m]) * 4u : kOob;
+      vo[m] = (unsigned)ix < (unsigned)W ? (unsigned)(ix * a.xp + dma_ch[m]) * 4u : kOob;
     }
   };
-  const unsigned row_bytes = (unsigned)W * kC * 4u;
+  const unsigned row_bytes = (unsigned)W * a.xp * 4u;   // one input row
+  const unsigned yrow_bytes = (unsigned)W * a.yp * 4u;  // one output (and residual) row
   // stage input row iy of image b into ring slot s: one descriptor per row (0 bytes for a
   // padding row), the lane offsets of its column group
   auto stage_row = [&](int b, int iy, int s, const unsigned (&vo)[3]) {
     const bool row_ok = (unsigned)iy < (unsigned)H;
-    const __amdgpu_buffer_rsrc_t rx = rsrc(a.x + ((size_t)b * H + (row_ok ? iy : 0)) * W * kC, row_ok ? row_bytes : 0u);
+    const __amdgpu_buffer_rsrc_t rx = rsrc(a.x + ((size_t)b * H + (row_ok ? iy : 0)) * W * a.xp, row_ok ? row_bytes : 0u);
 #pragma unroll
     for (int m = 0; m < 3; ++m) {
       if (m >= npiece) break;
@@ -318,7 +326,7 @@ __global__ __launch_bounds__(256, 1) void conv_wino_kernel(const WinoArgs a) {
     for (int j = 0; j < 2; ++j) {
       const int ox = 32 * g + 2 * t + j;
 #pragma unroll
-      for (int i = 0; i < 2; ++i) yo[i][j] = ox < W ? (unsigned)((i * W + ox) * kC + cbase) * 4u : kOob;
+      for (int i = 0; i < 2; ++i) yo[i][j] = ox < W ? (unsigned)((i * W + ox) * a.yp + cbase) * 4u : kOob;
     }
     if constexpr (POST == kPostPool) {
       const int px = 16 * g + t;
@@ -363,9 +371,9 @@ __global__ __launch_bounds__(256, 1) void conv_wino_kernel(const WinoArgs a) {
       // this lane's 4 output pixels in the finishing pass (channels 16 wave + 4 o .. +3): one
       // descriptor per item over its 2-row band (1 row at an odd image's last tile row); the
       // residual is loaded now so its latency hides behind the k-loop
-      const size_t band = ((size_t)cur.b * H + 2 * ty) * W * kC;
+      const size_t band = ((size_t)cur.b * H + 2 * ty) * W * a.yp;
       const unsigned band_rows = 2 * ty + 1 < H ? 2u : 1u;
-      const unsigned band_bytes = band_rows * row_bytes;
+      const unsigned band_bytes = band_rows * yrow_bytes;
       const __amdgpu_buffer_rsrc_t ry =
           POST == kPostTap ? rsrc(a.y + ((size_t)cur.b * H + 2 * ty) * W * a.pcp, band_rows * (unsigned)W * a.pcp * 4u)
                            : rsrc(a.y + band, band_bytes);
@@ -508,9 +516,10 @@ __global__ __launch_bounds__(256, 1) void conv_wino_kernel(const WinoArgs a) {
             const float ys = i == 0 ? (z[0][j][c] + z[1][j][c]) + z[2][j][c] : (z[1][j][c] - z[2][j][c]) - z[3][j][c];
             chk = fmaf(ys, 0.f, chk);
             float tv = fmaf(ys, a.osc, bj[c]);
+            if constexpr (RES == kResPre) tv += rv[i][j][c];
             if constexpr (ACT == FVC_ACT_RELU) tv = relu1(tv);
             if constexpr (ACT == FVC_ACT_LRELU) tv = fmaxf(tv, 0.1f * tv);
-            if constexpr (RES) tv += rv[i][j][c];
+            if constexpr (RES == kResPost) tv += rv[i][j][c];
             vv[c] = tv;
           }
           yv[i][j] = vv;
@@ -623,7 +632,7 @@ static int env_int(const char* n, int dflt) {
   return (v && v[0]) ? atoi(v) : dflt;
 }
 
-template <int IOP, int POST, bool RES, int ACT>
+template <int IOP, int POST, int RES, int ACT>
 static int wino_launch4(const WinoArgs& a, int grid, hipStream_t s) {
   const hipError_t e = hipFuncSetAttribute((const void*)conv_wino_kernel<IOP, POST, RES, ACT>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, kLds);
@@ -639,25 +648,40 @@ template <int IOP, int POST>
 static int wino_launch(const WinoArgs& a, int act, hipStream_t s, int grid) {
   if constexpr (POST == kPostTap && IOP != FVC_IN_NONE) return FVC_EINVAL;
   if (a.res) {
-    if (act == FVC_ACT_NONE) return wino_launch4<IOP, POST, true, FVC_ACT_NONE>(a, grid, s);
-    if (act == FVC_ACT_RELU) return wino_launch4<IOP, POST, true, FVC_ACT_RELU>(a, grid, s);
-    return wino_launch4<IOP, POST, true, FVC_ACT_LRELU>(a, grid, s);
+    if (act == FVC_ACT_NONE) return wino_launch4<IOP, POST, kResPost, FVC_ACT_NONE>(a, grid, s);
+    if (act == FVC_ACT_RELU) return wino_launch4<IOP, POST, kResPost, FVC_ACT_RELU>(a, grid, s);
+    return wino_launch4<IOP, POST, kResPost, FVC_ACT_LRELU>(a, grid, s);
   }
-  if (act == FVC_ACT_NONE) return wino_launch4<IOP, POST, false, FVC_ACT_NONE>(a, grid, s);
-  if (act == FVC_ACT_RELU) return wino_launch4<IOP, POST, false, FVC_ACT_RELU>(a, grid, s);
-  return wino_launch4<IOP, POST, false, FVC_ACT_LRELU>(a, grid, s);
+  if (act == FVC_ACT_NONE) return wino_launch4<IOP, POST, 0, FVC_ACT_NONE>(a, grid, s);
+  if (act == FVC_ACT_RELU) return wino_launch4<IOP, POST, 0, FVC_ACT_RELU>(a, grid, s);
+  return wino_launch4<IOP, POST, 0, FVC_ACT_LRELU>(a, grid, s);
 }
 
+// the second input half of a 128 -> 128 quarter pair: residual (the first half's partial sum)
+// added before the activation
+template <int IOP>
+static int wino_launch_pre(const WinoArgs& a, int act, hipStream_t s, int grid) {
+  if (act == FVC_ACT_NONE) return wino_launch4<IOP, 0, kResPre, FVC_ACT_NONE>(a, grid, s);
+  if (act == FVC_ACT_RELU) return wino_launch4<IOP, 0, kResPre, FVC_ACT_RELU>(a, grid, s);
+  return wino_launch4<IOP, 0, kResPre, FVC_ACT_LRELU>(a, grid, s);
+}
+
+// pitch = 128: x / y / res point at the first channel of a 64-channel half of 128-channel tensors;
+// res_pre adds res before the activation (bias may then be null: zeros)
 static int run_wino(const float* x, const void* upack, float osc, const float* bias, const float* res, float* y,
                     float* pool, int batch, int h, int w, int in_op, int act, int cu_reserve, int* ovf, int* sched,
-                    int sched_len, hipStream_t s, const void* tw = nullptr, float tosc = 0.f, int pcp = 0) {
+                    int sched_len, hipStream_t s, const void* tw = nullptr, float tosc = 0.f, int pcp = 0,
+                    int pitch = kC, bool res_pre = false) {
   if (tw && (pool || in_op != FVC_IN_NONE || pcp <= 0 || pcp > 32 || (pcp & 3))) return FVC_EINVAL;
-  if (!x || !upack || !bias || !y || batch <= 0 || h <= 0 || w <= 0 || cu_reserve < 0 || sched_len < 0)
+  if (!x || !upack || (!bias && pitch == kC) || !y || batch <= 0 || h <= 0 || w <= 0 || cu_reserve < 0 ||
+      sched_len < 0)
     return FVC_EINVAL;
+  if (pitch != kC && (pitch != 2 * kC || tw || pool)) return FVC_EINVAL;
+  if (res_pre && (!res || pitch != 2 * kC)) return FVC_EINVAL;
   if (in_op != FVC_IN_NONE && in_op != FVC_IN_RELU) return FVC_EINVAL;
   // every buffer descriptor spans one input row or one 2-row output band: 32-bit offsets hold
   // for any batch, only a band must stay below 4 GB
-  if ((unsigned long long)w * kC * 4ull * 2ull >= (1ull << 31)) return FVC_EINVAL;
+  if ((unsigned long long)w * pitch * 4ull * 2ull >= (1ull << 31)) return FVC_EINVAL;
   WinoArgs a;
   a.x = x;
   a.u = (const uint4*)upack;
@@ -679,12 +703,17 @@ static int run_wino(const float* x, const void* upack, float osc, const float* b
   a.tosc = tosc;
   a.tosc_c = tosc * (1.0f / 2048.f);
   a.pcp = pcp;
+  a.xp = a.yp = pitch;
   const int reserve = env_int("FVC_X3_RESERVE", -1) >= 0 ? env_int("FVC_X3_RESERVE", 0) : cu_reserve;
   const int ncu = wino_num_cus() - (reserve < wino_num_cus() / 2 ? reserve : wino_num_cus() / 2);
   int grid = ncu < a.nchunks ? ncu : a.nchunks;
   a.sched = (sched && sched_len >= 2 && env_int("FVC_X3_DYN", 1)) ? sched : nullptr;
   if (act != FVC_ACT_NONE && act != FVC_ACT_RELU && act != FVC_ACT_LRELU) return FVC_EINVAL;
   if (tw) return wino_launch<FVC_IN_NONE, kPostTap>(a, act, s, grid);
+  if (res_pre) {
+    if (in_op == FVC_IN_NONE) return wino_launch_pre<FVC_IN_NONE>(a, act, s, grid);
+    return wino_launch_pre<FVC_IN_RELU>(a, act, s, grid);
+  }
   if (pool) {
     if (in_op == FVC_IN_NONE) return wino_launch<FVC_IN_NONE, kPostPool>(a, act, s, grid);
     return wino_launch<FVC_IN_RELU, kPostPool>(a, act, s, grid);
@@ -795,6 +824,57 @@ int fvc_conv2d_nhwc_wino_tap(const float* x, const void* wpack, float osc, const
   if (!tap_wpack) return FVC_EINVAL;
   return run_wino(x, wpack, osc, bias, res, P, nullptr, batch, h, w, FVC_IN_NONE, act, cu_reserve, overflow_flag,
                   sched, sched_len, (hipStream_t)stream, tap_wpack, tap_osc, pcp);
+}
+
+int fvc_conv_wino128_supported(int cin, int cout, int ksize, int stride, int transposed) {
+  return cin == 2 * kC && cout == 2 * kC && ksize == 3 && stride == 1 && !transposed;
+}
+
+size_t fvc_conv_wino128_wpack_bytes(void) { return 4 * fvc_conv_wino_wpack_bytes(); }
+
+// w: [128][128][3][3] (OIHW) -> four 64 -> 64 packs, quarter (co half, ci half) at index
+// 2 * co_half + ci_half, each with its own scale (osc4[quarter])
+int fvc_conv_wino128_pack_weight(const float* w, void* wp, float* osc4) {
+  if (!w || !wp || !osc4) return FVC_EINVAL;
+  float* qw = (float*)malloc(sizeof(float) * kC * kC * 9);
+  if (!qw) return FVC_EINVAL;
+  for (int qd = 0; qd < 4; ++qd) {
+    const int oh = qd >> 1, ih = qd & 1;
+    for (int co = 0; co < kC; ++co)
+      for (int ci = 0; ci < kC; ++ci)
+        for (int k = 0; k < 9; ++k)
+          qw[((size_t)co * kC + ci) * 9 + k] = w[(((size_t)(kC * oh + co)) * 2 * kC + kC * ih + ci) * 9 + k];
+    const int r = fvc_conv_wino_pack_weight(qw, (char*)wp + qd * fvc_conv_wino_wpack_bytes(), osc4 + qd);
+    if (r) {
+      free(qw);
+      return r;
+    }
+  }
+  free(qw);
+  return 0;
+}
+
+// A 128 -> 128 3x3 stride-1 conv as four 64 -> 64 Winograd launches: per output half, the first
+// input half's sum (no bias, no activation) is written into y's half, then the second input half
+// adds bias and that partial sum before the activation (in place: each lane reads its residual
+// and writes the same bytes). Same stream order, no extra buffer.
+int fvc_conv2d_nhwc_wino128(const float* x, const void* wpack, const float* osc4, const float* bias, float* y,
+                            int batch, int h, int w, int in_op, int act, int cu_reserve, int* overflow_flag,
+                            int* sched, int sched_len, fvc_stream_t stream) {
+  if (!x || !wpack || !osc4 || !bias || !y) return FVC_EINVAL;
+  const size_t qb = fvc_conv_wino_wpack_bytes();
+  for (int oh = 0; oh < 2; ++oh) {
+    float* yh = y + kC * oh;
+    int r = run_wino(x, (const char*)wpack + (2 * oh) * qb, osc4[2 * oh], nullptr, nullptr, yh, nullptr, batch, h, w,
+                     in_op, FVC_ACT_NONE, cu_reserve, overflow_flag, sched, sched_len, (hipStream_t)stream, nullptr,
+                     0.f, 0, 2 * kC, false);
+    if (r) return r;
+    r = run_wino(x + kC, (const char*)wpack + (2 * oh + 1) * qb, osc4[2 * oh + 1], bias + kC * oh, yh, yh, nullptr,
+                 batch, h, w, in_op, act, cu_reserve, overflow_flag, sched, sched_len, (hipStream_t)stream, nullptr,
+                 0.f, 0, 2 * kC, true);
+    if (r) return r;
+  }
+  return 0;
 }
 
 int fvc_conv2d_nhwc_wino(const float* x, const void* wpack, float osc, const float* bias, const float* res,

@@ -273,7 +273,7 @@ class PackedConv:
         # per 4-frame launch (MI355X, r2). FVC_TAPSUM=0 / 2 disables / forces the tap path for
         # every eligible layer.
         self.tap = None
-        self.wino = self.dx = False
+        self.wino = self.dx = self.wino128 = False
         tapsum = os.environ.get("FVC_TAPSUM", "1")
         if (precision == "x3" and cout <= 4 and ksize in (3, 5) and stride == (2 if transposed else 1)
                 and cp4(cin) % 8 == 0 and tapsum != "0" and (tapsum == "2" or (cin >= 128 and not transposed))):
@@ -295,6 +295,15 @@ class PackedConv:
             uosc = ctypes.c_float(0.0)
             _lib.call("fvc_conv_wino_pack_weight", w.data_ptr(), upack.data_ptr(), ctypes.addressof(uosc))
             self.upack, self.uosc = upack.to(device), float(uosc.value)
+        # 128 -> 128 3x3 stride-1 layers (MV stacks): four 64 -> 64 Winograd quarters of the same
+        # kernel on 128-channel pixels (fvc_conv2d_nhwc_wino128); FVC_WINO128=0 keeps them direct
+        self.wino128 = (self.x3 and os.environ.get("FVC_WINO128", "1") != "0" and
+                        bool(lib.fvc_conv_wino128_supported(cin, cout, ksize, stride, int(transposed))))
+        if self.wino128:
+            q = torch.empty(lib.fvc_conv_wino128_wpack_bytes() // 2, dtype=torch.float16)
+            self.osc4 = (ctypes.c_float * 4)()
+            _lib.call("fvc_conv_wino128_pack_weight", w.data_ptr(), q.data_ptr(), ctypes.addressof(self.osc4))
+            self.upack128 = q.to(device)
         # stride-2 transposed layers on the all-classes kernel (fvc_deconv_x3.hip, conv_dx_kernel)
         self.dx = self.x3 and transposed and bool(lib.fvc_deconv_x3_all_classes(cin, cout, ksize, stride))
         if self.x3:
@@ -343,11 +352,22 @@ class PackedConv:
             ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             ev0.record()
         wino = self.wino and in_op in (IN_NONE, IN_RELU) and post == POST_NONE
+        # the quarters pay 4 launch tails: below ~0.5 M output pixels per launch (136x240 at 8 GOPs:
+        # 0.30 -> 0.42 ms) the direct kernel is faster; 272x480 even, 544x960 3.91 -> 3.23 ms (MI355X)
+        w128 = (self.wino128 and in_op in (IN_NONE, IN_RELU) and post == POST_NONE and res is None and
+                B * H * W >= int(os.environ.get("FVC_WINO128_MINPIX", "500000")))
         if wino:
             _lib.call("fvc_conv2d_nhwc_wino", x.data_ptr(), self.upack.data_ptr(), self.uosc, self.bias.data_ptr(),
                       _ptr(res), y.data_ptr(), None, B, H, W, in_op, act, _STATE["cu_reserve"],
                       overflow_flag(x.device).data_ptr(), sched_scratch(x.device).data_ptr(), SCHED_LEN,
                       stream_handle())
+        elif w128:
+            import ctypes
+            _lib.call("fvc_conv2d_nhwc_wino128", x.data_ptr(), self.upack128.data_ptr(), ctypes.addressof(self.osc4),
+                      self.bias.data_ptr(), y.data_ptr(), B, H, W, in_op, act, _STATE["cu_reserve"],
+                      overflow_flag(x.device).data_ptr(), sched_scratch(x.device).data_ptr(), SCHED_LEN,
+                      stream_handle())
+            wino = True
         elif self.x3:
             fn = "fvc_deconv2d_nhwc_x3" if self.transposed else "fvc_conv2d_nhwc_x3"
             _lib.call(fn, x.data_ptr(), self.wpack.data_ptr(), self.osc, self.bias.data_ptr(), _ptr(res),

@@ -164,6 +164,18 @@ int fvc_conv2d_nhwc_wino_tap(const float* x, const void* wpack, float osc, const
                              const float* res, float* P, int batch, int h, int w, int act,
                              const void* tap_wpack, float tap_osc, int pcp, int cu_reserve,
                              int* overflow_flag, int* sched, int sched_len, fvc_stream_t stream);
+/* The 128 -> 128 3x3 stride-1 layers (MV analysis/synthesis conv2/4/6/8, analysis_mv.py:58-66,
+ * synthesis_mv.py:59-79; in_op none / relu, act, no residual) as four 64 -> 64 Winograd quarters
+ * of the same kernel on 128-channel pixels: per output half the first input half's sum goes into
+ * y's half, then the second input half adds bias and that partial sum before the activation.
+ * wpack: fvc_conv_wino128_wpack_bytes() bytes from fvc_conv_wino128_pack_weight (w OIHW
+ * [128][128][3][3]); osc4: the four quarter scales (host floats). */
+int fvc_conv_wino128_supported(int cin, int cout, int ksize, int stride, int transposed);
+size_t fvc_conv_wino128_wpack_bytes(void);
+int fvc_conv_wino128_pack_weight(const float* w_host, void* wpack_host, float* osc4_out);
+int fvc_conv2d_nhwc_wino128(const float* x, const void* wpack, const float* osc4_host, const float* bias,
+                            float* y, int batch, int h, int w, int in_op, int act, int cu_reserve,
+                            int* overflow_flag, int* sched, int sched_len, fvc_stream_t stream);
 
 /* ------------------------------------------------------------------ layout / resampling */
 int fvc_nchw_to_nhwc(const float* src, float* dst, int batch, int c, int h, int w, int cp,

@@ -196,3 +196,59 @@ def test_wino_tap_epilogue(dev, shape, monkeypatch):
     print(f"{shape}: wino tap err {ew / scale:.2e}, direct tap err {ed / scale:.2e} (of output scale)")
     assert ew <= 2e-6 * scale, (ew, ed, scale)
     assert float(out_w[..., 3:].abs().max()) == 0.0
+
+
+# (B, H, W, in_op, act): the MV stacks' 128 -> 128 3x3 stride-1 forms (analysis_mv.py:58-66,
+# synthesis_mv.py:59-79: ReLU act, conv8 none), sizes cut at every edge
+CASES128 = [
+    (2, 17, 30, K.IN_NONE, K.ACT_RELU),
+    (1, 34, 60, K.IN_NONE, K.ACT_NONE),
+    (3, 9, 70, K.IN_RELU, K.ACT_LRELU),
+    (1, 40, 33, K.IN_NONE, K.ACT_RELU),
+]
+
+
+@pytest.mark.parametrize("case", CASES128, ids=lambda c: f"b{c[0]}_{c[1]}x{c[2]}_io{c[3]}_a{c[4]}")
+def test_wino128_quarters_vs_float64_and_direct(dev, case, monkeypatch):
+    """fvc_conv2d_nhwc_wino128 (four 64 -> 64 Winograd quarters on 128-channel pixels, the second
+    input half adding the first's partial sum before the activation) against float64 torch and the
+    direct x3 kernel (FVC_WINO128=0); determinism; the overflow flag stays clear."""
+    B, H, W, in_op, act = case
+    g = torch.Generator().manual_seed(B * 1000 + H * W + act)
+    w = torch.randn(128, 128, 3, 3, generator=g) * (1.0 / (128 * 9) ** 0.5)
+    b = torch.randn(128, generator=g) * 0.1
+    x = torch.randn(B, 128, H, W, generator=g) * 2
+    xr = torch.relu(x) if in_op == K.IN_RELU else x
+    ref = F.conv2d(xr.double(), w.double(), b.double(), 1, 1)
+    ref = {K.ACT_NONE: ref, K.ACT_RELU: torch.relu(ref), K.ACT_LRELU: F.leaky_relu(ref, 0.1)}[act]
+    monkeypatch.setenv("FVC_WINO128_MINPIX", "0")  # test sizes are below the production gate
+    monkeypatch.setenv("FVC_WINO128", "1")
+    pw = K.PackedConv(w, b, 3, 1, False, dev, precision="x3")
+    monkeypatch.setenv("FVC_WINO128", "0")
+    pd = K.PackedConv(w, b, 3, 1, False, dev, precision="x3")
+    assert pw.wino128 and not pd.wino128 and pd.x3
+    xd = to_nhwc(x).to(dev)
+    K.x3_overflow(reset=True)
+    yw = pw(xd, in_op=in_op, act=act)
+    yw2 = pw(xd, in_op=in_op, act=act)
+    yd = pd(xd, in_op=in_op, act=act)
+    torch.cuda.synchronize()
+    assert not K.x3_overflow(reset=True)
+    assert torch.equal(yw, yw2)
+    assert not torch.equal(yw, yd)  # two algorithms ran
+    scale = float(ref.abs().max())
+    ew = float((from_nhwc(yw.cpu()).double() - ref).abs().max())
+    ed = float((from_nhwc(yd.cpu()).double() - ref).abs().max())
+    print(f"{case}: wino128 {ew / scale:.2e}, direct {ed / scale:.2e} of output scale")
+    assert ew <= 1e-6 * scale and ew <= 2 * ed + 1e-7 * scale, (ew, ed, scale)
+
+
+def test_wino128_rejects_residual_and_wrong_pitch_forms():
+    """The quarter form takes no residual (PackedConv keeps such calls on the direct kernel) and
+    the C-ABI refuses null buffers."""
+    from fastvideocodec_amd import _lib
+    lib = _lib.load()
+    assert lib.fvc_conv_wino128_supported(128, 128, 3, 1, 0) == 1
+    assert lib.fvc_conv_wino128_supported(128, 128, 3, 2, 0) == 0
+    assert lib.fvc_conv_wino128_supported(64, 64, 3, 1, 0) == 0
+    assert lib.fvc_conv2d_nhwc_wino128(None, None, None, None, None, 1, 4, 4, 0, 0, 0, None, None, 0, None) < 0
