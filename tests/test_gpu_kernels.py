@@ -387,6 +387,27 @@ def test_upsample_add(dev, ac, scale):
     assert torch.equal(y68[..., :64], y)
 
 
+@pytest.mark.parametrize("shape", [(2, 9, 15), (1, 1, 1), (1, 1, 7), (3, 6, 1), (1, 34, 60)])
+@pytest.mark.parametrize("with_skip", [False, True])
+def test_upsample_64ch_forms_bit_identical(dev, shape, with_skip, monkeypatch):
+    """The 64-channel upsample-add forms (FVC_UP2_Q16: 1 = 32-bit-index float4 per thread, 0 =
+    generic) give the same bits, including images of one source row / column, and match the oracle."""
+    B, h, w = shape
+    g = torch.Generator().manual_seed(h * 100 + w)
+    src = to_nhwc(torch.randn(B, 64, h, w, generator=g)).to(dev)
+    skip = to_nhwc(torch.randn(B, 64, 2 * h, 2 * w, generator=g)).to(dev) if with_skip else None
+    outs = []
+    for form in ("1", "0"):
+        monkeypatch.setenv("FVC_UP2_Q16", form)
+        outs.append(K.upsample2x_add(src, skip, align_corners=False, scale=1.0))
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+    ref = dvc_ref.up2(from_nhwc(src.cpu(), 64), False)
+    if skip is not None:
+        ref = from_nhwc(skip.cpu(), 64) + ref
+    close(from_nhwc(outs[0].cpu(), 64), ref, 1e-6)
+
+
 def test_avgpool(dev):
     x = torch.randn(2, 64, 18, 34)
     y = K.avgpool2(to_nhwc(x).to(dev))
