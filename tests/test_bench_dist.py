@@ -111,6 +111,17 @@ def test_bench_gpus2_spawns_two_ranks(tmp_path):
     assert dt >= 2 * 0.010 * 0.9                    # rank 1's 10 ms steps bound the time
 
 
+def test_bench_gpus4_gop32_one_gop_per_rank(tmp_path):
+    """BASELINE configs[3]'s layout (`--gpus 4 --gop 32 --gops-per-gpu 1`): GOP r on rank r, 31
+    P-frames per GOP counted over all four ranks."""
+    res = _run_bench_cli(["--gpus", "4", "--gop", "32", "--gops-per-gpu", "1", "--steps", "1", "--warmup", "0",
+                          "--height", "64", "--width", "128"], tmp_path)
+    assert res["n_gpus"] == 4 and res["config"]["parallelism"] == "gop-shard x4"
+    assert res["shards"] == {"unit": "gop", "by_rank": [[0], [1], [2], [3]]}
+    assert res["quality"]["bitstreams_gathered_to_rank0_bytes"] == sum(100 + g for g in range(4))
+    assert abs(res["value"] * res["ms_per_step"] / 1e3 - 4 * 31) < 1e-3 * 4 * 31  # (rounded fields)
+
+
 def test_bench_views8_gpus8_view_v_on_rank_v(tmp_path):
     """BASELINE configs[4]: `--views 8 --gpus 8` puts view v on rank v."""
     res = _run_bench_cli(["--gpus", "8", "--views", "8", "--steps", "1", "--warmup", "0",

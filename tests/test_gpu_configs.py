@@ -135,3 +135,28 @@ def test_views8_1080p_config4(dev):
     sse_cpu = float(((o_clip - cur) ** 2).sum())
     dpsnr = abs(10 * np.log10(sse_cpu / sse_gpu))
     assert dpsnr <= 1e-4, dpsnr
+
+
+def test_gop32_four_rank_split(dev):
+    """BASELINE configs[3]'s GOP structure (GOP-32: 31 P-frames per I-frame, one GOP per rank over
+    4 ranks), at a small frame size, with the ranks' jobs run one after the other on this GPU: rank r
+    codes GOP r (the same frames as GOP r of a one-rank job with 4 GOPs), every rank's decoder is
+    bit-exact over all 31 P-frames without split-precision overflow, and the four ranks' payloads
+    add up to the one-rank job's."""
+    import bench
+    from fastvideocodec_amd import kernels as K
+
+    one = bench.GpuGopJob(_args(gop=32, gops_per_gpu=4, height=64, width=96), 0, 1, dev)
+    assert one.units == 4 and tuple(one.frames.shape[:2]) == (4, 32)
+    v_one = one.verify()
+    assert v_one["bitexact"] and v_one["overflow_recomputes"] == 0
+    total = 0
+    for r in range(4):
+        job = bench.GpuGopJob(_args(gop=32, gops_per_gpu=1, height=64, width=96), r, 4, dev)
+        assert job.shard == [r] and job.units == 1
+        np.testing.assert_array_equal(job.gops_np[0], one.gops_np[r])
+        K.x3_overflow(reset=True)
+        v = job.verify()
+        assert v["bitexact"] and v["overflow_recomputes"] == 0 and not K.x3_overflow(reset=True)
+        total += v["nbytes"]
+    assert total == v_one["nbytes"]
