@@ -39,6 +39,8 @@ CASES = {
     "c1_64_75_half": (64, 75, 1, 1, False, 544, 960),
     # Warp_net ResBlock second conv: relu on the input, residual add in the epilogue
     "c3_64_full_res": (64, 64, 3, 1, False, 1088, 1920, "res"),
+    "c3_64_full_relu": (64, 64, 3, 1, False, 1088, 1920, "relu"),   # ResBlock conv1: ReLU in, ReLU act
+    "c3_64_half_relu": (64, 64, 3, 1, False, 544, 960, "relu"),
     "c3_64_half_res": (64, 64, 3, 1, False, 544, 960, "res"),
 }
 
@@ -50,7 +52,8 @@ args = ap.parse_args()
 dev = torch.device("cuda")
 for name in args.cases.split(","):
     cin, cout, k, s, tr, H, W = CASES[name][:7]
-    with_res = len(CASES[name]) > 7
+    form = CASES[name][7] if len(CASES[name]) > 7 else ""
+    with_res = form == "res"
     if tr:
         H, W = H // 2, W // 2
     w = torch.randn((cin, cout, k, k) if tr else (cout, cin, k, k)) * 0.05
@@ -60,6 +63,8 @@ for name in args.cases.split(","):
     kw = {}
     if with_res:
         kw = dict(in_op=K.IN_RELU, res=torch.randn(B, *pc.out_hw(H, W), K.cp4(cout), device=dev))
+    elif form == "relu":
+        kw = dict(in_op=K.IN_RELU, act=K.ACT_RELU)
     y = pc(x, **kw)
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
