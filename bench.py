@@ -472,7 +472,8 @@ def roofline_fields(prof, job, args):
                      "kernel": "split-precision conv kernels (every conv launch but 4 small-cin layers): "
                                "conv_x3_kernel (fp16x3 implicit-GEMM conv/deconv) + conv_dx_kernel (stride-2 "
                                "transposed convs, all parity classes per staged tile) + conv_wino_kernel (Winograd "
-                               "F(2x2,3x3) for the 64->64 3x3 layers), all their launches",
+                               "F(2x2,3x3) for the 64->64 3x3 layers, and the 544x960 128->128 ones as four 64->64 "
+                               "quarters), all their dispatches",
                      "achieved_is": "algorithmic fp32-conv FLOP (2 x MAC of the direct convolution) / kernel time; "
                                     "the direct kernel issues 3 f16 MFMAs per MAC (ceiling peak/3), the Winograd "
                                     "kernel 3 per 16/36 MAC (ceiling peak/3 x 36/16)",

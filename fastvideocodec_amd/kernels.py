@@ -387,8 +387,10 @@ class PackedConv:
             timer.records.append((ev0, ev1, profiling.conv_flops(self.cin, self.cout, self.ksize, self.stride,
                                                                  self.transposed, B, H, W),
                                   f"{'deconv' if self.transposed else 'conv'}{self.ksize}s{self.stride} "
-                                  f"{self.cin}->{self.cout} @{H}x{W}{' wino' if wino else (' dx' if self.dx else (' x3' if self.x3 else ''))}",
-                                  self.x3, nbytes, "wino" if wino else ("dx" if self.dx else ("x3" if self.x3 else "f32"))))
+                                  f"{self.cin}->{self.cout} @{H}x{W}{' wino' if wino else (' dx' if self.dx else (' x3' if self.x3 else ''))}"
+                                  f"{' x4' if w128 else ''}",
+                                  self.x3, nbytes, "wino" if wino else ("dx" if self.dx else ("x3" if self.x3 else "f32")),
+                                  4 if w128 else 1))  # kernel dispatches (the quarters are 4)
         return y
 
 

@@ -41,12 +41,13 @@ class KernelTimer:
     def collect(self, x3=None, family=None):
         """Synchronise and return (total_ms, total_flops, n_launches); x3=True/False restricts to
         the split-precision / the fp32+VALU conv launches, family to one kernel ('x3': the direct
-        conv_x3_kernel, 'wino': conv_wino_kernel, 'f32')."""
+        conv_x3_kernel, 'wino': conv_wino_kernel, 'f32'). n_launches counts kernel dispatches (a
+        record's 8th field; the 128-channel Winograd quarters are 4 per call), as rocprofv3 does."""
         torch.cuda.synchronize()
         rs = self._select(x3, family)
         ms = sum(r[0].elapsed_time(r[1]) for r in rs)
         fl = sum(r[2] for r in rs)
-        return ms, fl, len(rs)
+        return ms, fl, sum(r[7] if len(r) > 7 else 1 for r in rs)
 
     def collect_bytes(self, x3=None, family=None):
         """Algorithmic HBM bytes (input + packed weights + output + residual) of the launches
