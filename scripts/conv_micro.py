@@ -22,6 +22,7 @@ CASES = {
     "d5_64_quarter": (64, 64, 5, 2, True, 272, 480),
     "d5_96_64_16": (96, 64, 5, 2, True, 136, 240),
     "c7_32_16_full": (32, 16, 7, 1, False, 1088, 1920),
+    "c7_64_32_full": (64, 32, 7, 1, False, 1088, 1920),
     "c3_64_half": (64, 64, 3, 1, False, 544, 960),
     "c3_128_quarter": (128, 128, 3, 1, False, 272, 480),
     "c3_128_eighth": (128, 128, 3, 1, False, 136, 240),
