@@ -62,6 +62,9 @@ constexpr int kHdr = 512;                             // bias (256 B) + schedule
 constexpr int kLds = kHdr + kRingBytes + 2 * kZBytes; // 148,480 B
 constexpr int kChunk = 16;         // items per schedule chunk (consecutive tile rows of one column)
 constexpr float kLoScale = 2048.f;
+#ifndef FVC_WINO_KO_WAIT
+#define FVC_WINO_KO_WAIT 0
+#endif
 #ifndef FVC_WINO_ALLNOP
 #define FVC_WINO_ALLNOP 0
 #endif
@@ -493,7 +496,11 @@ __global__ __launch_bounds__(256, 1) void conv_wino_kernel(const WinoArgs a) {
         *reinterpret_cast<f32x4*>(zw + ((wave * 2 + 0) * 4 + n) * 1024 + lane * 16) = z0;
         *reinterpret_cast<f32x4*>(zw + ((wave * 2 + 1) * 4 + n) * 1024 + lane * 16) = z1;
       }
+#if FVC_WINO_KO_WAIT
+      asm volatile("" ::: "memory");  // knock-out (experiment builds only): no wait for the next item's rows
+#else
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA pieces of the next item
+#endif
       __syncthreads();
       if (first) nnp = decode(sq[2 + (ntaken & 1)]);  // published by this item's barrier
 
