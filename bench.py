@@ -1,7 +1,7 @@
 """1080p DVC P-frame encode+decode throughput on MI355X (BASELINE.json metric, configs[2]).
 
-A step = G GOP-12s per GPU batched along dim 0 (G = --gops-per-gpu, default 8; default 2 timed
-steps = 16 GOPs per run), one GOP per batch slot, at 1920x1080
+A step = G GOP-12s per GPU batched along dim 0 (G = --gops-per-gpu, default 16; default 2 timed
+steps = 32 GOPs per run), one GOP per batch slot, at 1920x1080
 (replicate-padded to 1920x1088): frame 0 is the I-frame (passed through; BPG is out of scope),
 frames 1..11 are DVC P-frames, each encoded (full encoder forward incl. its reconstruction, then
 rANS range coding of mv / z / feature into a bitstream) and decoded (rANS decode -> hyperprior ->
@@ -460,7 +460,7 @@ def roofline_fields(prof, job, args):
     x3_bytes = prof["x3_bytes"]
     nfr = job.units * (args.gop - 1)
     achieved = x3_flops / (x3_ms * 1e-3) / 1e12 if x3_ms > 0 else 0.0
-    pmc = load_pmc_traffic(args.height, args.width)
+    pmc = load_pmc_traffic(args.height, args.width, job.units)
     return {
         "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": F16_MFMA_PEAK_TFLOPS,
                      "unit": "TFLOP/s", "frac": round(achieved / F16_MFMA_PEAK_TFLOPS, 4),
@@ -514,7 +514,7 @@ def per_kernel_fields(prof, nfr):
     return out
 
 
-def load_pmc_traffic(H, W):
+def load_pmc_traffic(H, W, gops):
     """HBM bytes per conv_x3_kernel launch from the committed rocprofv3 FETCH_SIZE/WRITE_SIZE passes
     over `bench.py --serial` (profiles/<round>/x3_traffic.json, written by scripts/rocprof_summary.py;
     FETCH_SIZE doubled per MI355X_MICROARCH.md's gfx950 correction). PMC passes serialise every
@@ -526,11 +526,13 @@ def load_pmc_traffic(H, W):
                 d = json.load(f)
         except (OSError, ValueError):
             continue
-        if d.get("height") != H or d.get("width") != W:
+        # per-dispatch bytes depend on the batch: only a file profiled at this GOP count counts
+        # (files without the field were profiled at 8)
+        if d.get("height") != H or d.get("width") != W or d.get("gops_per_gpu", 8) != gops:
             continue
         return {"hbm_bytes_per_launch": d.get("hbm_bytes_per_launch"),
                 "source": f"profiles/{rnd}/x3_traffic.json (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, "
-                          f"{d.get('launches')} launches)"}
+                          f"{d.get('launches')} dispatches at {gops} GOPs per step)"}
     return {}
 
 
@@ -542,10 +544,11 @@ def parse_args(argv=None):
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--gop", type=int, default=12)
-    ap.add_argument("--gops-per-gpu", type=int, default=8,
-                    help="GOPs batched per rank per step (SURVEY §8(e)); default 8 x 2 steps = 16 GOPs per run "
-                         "(§8(d)). Measured on MI355X (r2, fused epilogues, 3 steps): 4 -> 56.1/56.2, "
-                         "6 -> 56.9, 8 -> 58.2/58.9/58.7, 12 -> 58.8, 16 -> 59.3 P-frames/s")
+    ap.add_argument("--gops-per-gpu", type=int, default=16,
+                    help="GOPs batched per rank per step (SURVEY §8(e)); default 16 x 2 steps = 32 GOPs per run "
+                         "(§8(d)). Measured on MI355X (3 steps): r2 4 -> 56.1, 8 -> 58.2-58.9, 16 -> 59.3; r3 "
+                         "8 -> 68.92/68.84, 16 -> 69.92/69.95/69.91, 24 -> 68.13, 32 -> 68.22 P-frames/s "
+                         "(profiles/r3/gops_sweep)")
     ap.add_argument("--views", type=int, default=0,
                     help="BASELINE configs[4]: V camera views, one GOP stream each, view v -> rank v %% world "
                          "(replaces --gops-per-gpu; the reference's MCVC couples views, DVC views are independent)")

@@ -41,6 +41,7 @@ def main():
     ap.add_argument("--json-out")
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--gops-per-gpu", type=int, default=16, help="the profiled bench's GOPs per step")
     a = ap.parse_args()
     nframes = a.nframes
     rows = list(csv.DictReader(open(a.stats)))
@@ -66,7 +67,7 @@ def main():
     if a.fetch and a.write:
         # gfx950: FETCH_SIZE tallies 128-B requests at 64 B -> x2 (MI355X_MICROARCH.md, HBM section);
         # WRITE_SIZE exact for 16-B-per-lane stores (the x3 epilogue stores float4)
-        out = {"height": a.height, "width": a.width,
+        out = {"height": a.height, "width": a.width, "gops_per_gpu": a.gops_per_gpu,
                "correction": "FETCH_SIZE x2 (gfx950 wide-read tally), WRITE_SIZE x1"}
         fam_f, fam_w = {}, {}
         for k in SPLIT:
