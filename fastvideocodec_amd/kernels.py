@@ -249,6 +249,20 @@ class OverflowProbe:
         return bool(self.host.item())
 
 
+def x3_dispatches(batch, y_image_bytes, res_image_bytes=0):
+    """Kernel dispatches of one split-precision direct / all-classes conv call: the C-ABI halves the
+    batch recursively while the output (or residual) reaches 4 GB (32-bit buffer offsets,
+    fvc_conv_x3.hip run_x3), so the timer counts dispatches as rocprofv3 does. The Winograd kernel
+    never splits."""
+    split_at = int(os.environ.get("FVC_X3_SPLIT_BYTES", "0") or 0) or (1 << 32) - 4096
+
+    def n(b):
+        if b > 1 and (b * y_image_bytes >= split_at or b * res_image_bytes >= split_at):
+            return n(b // 2) + n(b - b // 2)
+        return 1
+    return n(batch)
+
+
 class PackedConv:
     """A conv / transposed conv with weights packed once for its HIP kernel: the split-precision
     fp16 x3 kernel where supported (cin padded to a multiple of 8, cout > 4), else fp32 MFMA /
@@ -390,7 +404,9 @@ class PackedConv:
                                   f"{self.cin}->{self.cout} @{H}x{W}{' wino' if wino else (' dx' if self.dx else (' x3' if self.x3 else ''))}"
                                   f"{' x4' if w128 else ''}",
                                   self.x3, nbytes, "wino" if wino else ("dx" if self.dx else ("x3" if self.x3 else "f32")),
-                                  4 if w128 else 1))  # kernel dispatches (the quarters are 4)
+                                  4 if w128 else (1 if wino or not self.x3 else
+                                                  x3_dispatches(B, 4 * y[0].numel(),
+                                                                4 * res[0].numel() if res is not None else 0))))
         return y
 
 
@@ -430,7 +446,9 @@ class PackedConv:
                 self.wpack.numel() * self.wpack.element_size()
             timer.records.append((ev0, ev1, profiling.conv_flops(self.cin, self.cout, self.ksize, 1, False, B, H, W),
                                   f"conv{self.ksize}s1 {self.cin}->{self.cout} @{H}x{W} {'wino' if self.wino else 'x3'} +pool",
-                                  True, nbytes, "wino" if self.wino else "x3"))
+                                  True, nbytes, "wino" if self.wino else "x3",
+                                  1 if self.wino else x3_dispatches(B, 4 * y[0].numel(),
+                                                                    4 * res[0].numel() if res is not None else 0)))
         return y, pool
 
     def _wino_tap(self, tap: "TapConsumer") -> bool:
@@ -488,7 +506,9 @@ class PackedConv:
             timer.records.append((ev0, ev1, fl, f"{'deconv' if self.transposed else 'conv'}{self.ksize}s{self.stride} "
                                   f"{self.cin}->{self.cout} @{H}x{W} {'wino' if wino else ('dx' if self.dx else 'x3')} "
                                   f"+tap{tap.ksize}x{tap.ksize}->{tap.cout}", True, nbytes,
-                                  "wino" if wino else ("dx" if self.dx else "x3")))
+                                  "wino" if wino else ("dx" if self.dx else "x3"),
+                                  1 if wino else x3_dispatches(B, 4 * P[0].numel(),
+                                                               4 * res[0].numel() if res is not None else 0)))
         return P
 
 

@@ -183,3 +183,19 @@ def test_bench_bookkeeping():
     assert bench.metric_name(1080, 1920) == "1080p frames/sec encode+decode at λ=1024; bpp/PSNR parity vs CPU ref"
     assert bench.metric_name(2160, 3840).startswith("3840x2160 ")
     assert 1 <= bench.cpu_cores() <= len(os.sched_getaffinity(0))
+
+
+def test_x3_dispatch_count_mirrors_the_batch_split(monkeypatch):
+    """The timer's dispatch count follows run_x3's recursive halving at 4 GB of output / residual
+    (so bench avg_launch_us is per kernel dispatch, as rocprofv3 counts)."""
+    from fastvideocodec_amd.kernels import x3_dispatches
+    monkeypatch.delenv("FVC_X3_SPLIT_BYTES", raising=False)
+    full64 = 1088 * 1920 * 64 * 4
+    assert x3_dispatches(8, full64) == 1          # 4.28 GB < 4 GB - 4 KB: one launch
+    assert x3_dispatches(16, full64) == 2
+    assert x3_dispatches(3, 2176 * 3840 * 64 * 4) == 2
+    assert x3_dispatches(1, 1 << 40) == 1         # one image never splits (the C side refuses it)
+    assert x3_dispatches(4, 100, res_image_bytes=1 << 31) == 4
+    monkeypatch.setenv("FVC_X3_SPLIT_BYTES", "1000")
+    assert x3_dispatches(5, 300) == 2             # 1500 B -> 2 + 3 images (600, 900 B): two launches
+    assert x3_dispatches(8, 300) == 4             # 2400 -> 4 + 4 (1200 each) -> 2 + 2 + 2 + 2
