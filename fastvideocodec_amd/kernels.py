@@ -7,6 +7,7 @@ kernels trust their arguments (an out-of-bounds launch can fault the whole GPU).
 from __future__ import annotations
 
 import contextlib
+import ctypes
 import os
 
 import torch
@@ -270,7 +271,6 @@ class PackedConv:
 
     def __init__(self, weight: torch.Tensor, bias: torch.Tensor, ksize: int, stride: int, transposed: bool,
                  device, precision: str | None = None):
-        import ctypes
         lib = _lib.load()
         w = weight.detach().to("cpu", torch.float32).contiguous()
         if transposed:
@@ -378,7 +378,6 @@ class PackedConv:
                       overflow_flag(x.device).data_ptr(), sched_scratch(x.device).data_ptr(), SCHED_LEN,
                       stream_handle())
         elif w128:
-            import ctypes
             _lib.call("fvc_conv2d_nhwc_wino128", x.data_ptr(), self.upack128.data_ptr(), ctypes.addressof(self.osc4),
                       self.bias.data_ptr(), y.data_ptr(), B, H, W, in_op, act, _STATE["cu_reserve"],
                       overflow_flag(x.device).data_ptr(), sched_scratch(x.device).data_ptr(), SCHED_LEN,
@@ -521,7 +520,6 @@ class TapConsumer:
     (deconv7 -> deconv8) and endecoder.py:278-279 (Warp_net conv5 -> conv6)."""
 
     def __init__(self, weight: torch.Tensor, bias: torch.Tensor, ksize: int, stride: int, transposed: bool, device):
-        import ctypes
         lib = _lib.load()
         w = weight.detach().to("cpu", torch.float32).contiguous()
         cin, cout = (w.shape[0], w.shape[1]) if transposed else (w.shape[1], w.shape[0])
@@ -570,7 +568,6 @@ class GdnTap:
     igdn3 -> deconv4 (synthesis.py:26,57; 64 -> 3, 5x5 s2, 75 partials)."""
 
     def __init__(self, weight: torch.Tensor, bias: torch.Tensor, ksize: int, stride: int, transposed: bool, device):
-        import ctypes
         lib = _lib.load()
         w = weight.detach().to("cpu", torch.float32).contiguous()
         cin, cout = (w.shape[0], w.shape[1]) if transposed else (w.shape[1], w.shape[0])
@@ -596,7 +593,6 @@ class GdnTap:
 
     def __call__(self, x, beta, gamma, inverse, act=ACT_NONE, post=POST_NONE, res=None):
         """consumer(gdn(x)) without writing gdn(x)."""
-        import ctypes
         B, H, W, C = x.shape
         if C != 64:
             raise ValueError("GDN + tap needs 64 channels")
