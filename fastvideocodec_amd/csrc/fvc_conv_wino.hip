@@ -43,6 +43,12 @@
 
 namespace {
 
+// cache policy of the activation stores (aux operand of buffer_store; experiment builds only,
+// e.g. 2 = non-temporal on gfx950)
+#ifndef FVC_STORE_AUX
+#define FVC_STORE_AUX 0
+#endif
+
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f2v __attribute__((ext_vector_type(2)));
@@ -531,7 +537,7 @@ __global__ __launch_bounds__(256, 1) void conv_wino_kernel(const WinoArgs a) {
           }
           yv[i][j] = vv;
           if constexpr (POST != kPostTap)
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, vv), ry, yo[i][j], 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, vv), ry, yo[i][j], 0, FVC_STORE_AUX);
         }
       if constexpr (POST == kPostPool) {
         f32x4 pv;

@@ -44,6 +44,12 @@
 
 namespace {
 
+// cache policy of the activation stores (aux operand of buffer_store; experiment builds only,
+// e.g. 2 = non-temporal on gfx950)
+#ifndef FVC_STORE_AUX
+#define FVC_STORE_AUX 0
+#endif
+
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 
 constexpr int kMaxTapsX = 49;
@@ -759,7 +765,7 @@ __global__ __launch_bounds__(NWV * 64) void conv_x3_kernel(const X3Args a) {
         }
         const unsigned so = (row_ok && j0 < a.coutp) ? vo + 32u * g : kOob;
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, make_float4(v[0], v[1], v[2], v[3])),
-                                               ry, so, 0, 0);
+                                               ry, so, 0, FVC_STORE_AUX);
         if constexpr (POST == kPostPool) {
           if (m == 0) {
 #pragma unroll

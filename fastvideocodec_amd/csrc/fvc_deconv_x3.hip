@@ -24,6 +24,12 @@
 #include <math.h>
 
 namespace fvc_dx {
+
+// cache policy of the activation stores (aux operand of buffer_store; experiment builds only,
+// e.g. 2 = non-temporal on gfx950)
+#ifndef FVC_STORE_AUX
+#define FVC_STORE_AUX 0
+#endif
 namespace {
 
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
@@ -424,7 +430,7 @@ __global__ __launch_bounds__(kNT) void conv_dx_kernel(const DxArgs a) {
               }
               const unsigned so = (ok && j0 < a.coutp && !(kKO & 16)) ? vo + 32u * g : kOob;
               __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, make_float4(v[0], v[1], v[2], v[3])),
-                                                     ry, so, 0, 0);
+                                                     ry, so, 0, FVC_STORE_AUX);
             }
           }
         }
