@@ -367,11 +367,12 @@ class PackedConv:
             ev0.record()
         wino = self.wino and in_op in (IN_NONE, IN_RELU) and post == POST_NONE
         # the quarters pay 4 launch tails: at 16 GOPs per launch 136x240 0.58 -> 0.62 ms, 272x480
-        # 1.97 -> 1.72, 544x960 7.46 -> 6.08 (MI355X, profiles/r3/wino128), so images of >= 100 K
-        # pixels take them. Gated per image, not per launch: a frame's result must not depend on
-        # how many frames share its batch.
+        # 1.97 -> 1.72, 544x960 7.46 -> 6.08 (MI355X, profiles/r3/wino128); images of >= 200 K
+        # pixels take them (a 100 K gate adding 272x480 measured bench-neutral: 70.91 / 70.96 vs
+        # 71.08 / 70.89). Gated per image, not per launch: a frame's result must not depend on how
+        # many frames share its batch.
         w128 = (self.wino128 and in_op in (IN_NONE, IN_RELU) and post == POST_NONE and res is None and
-                H * W >= int(os.environ.get("FVC_WINO128_MINPIX", "100000")))
+                H * W >= int(os.environ.get("FVC_WINO128_MINPIX", "200000")))
         if wino:
             _lib.call("fvc_conv2d_nhwc_wino", x.data_ptr(), self.upack.data_ptr(), self.uosc, self.bias.data_ptr(),
                       _ptr(res), y.data_ptr(), None, B, H, W, in_op, act, _STATE["cu_reserve"],
