@@ -15,13 +15,16 @@ Consecutive steps are pipelined the way a streaming encoder runs: a GOP's coder/
 (encode_decode_gop(join=False)); the timer stops after a device-wide synchronize, so all work of
 all K GOPs is inside the timed region.
 
-Multi-GPU: one process per GPU (torchrun), GOPs sharded by rank, no data-path collective;
-RCCL is used only after timing (max-time all_reduce, per-rank stats all_gather, bitstreams
-gathered to rank 0).
+Multi-GPU: one process per GPU, either under a launcher (torchrun sets WORLD_SIZE) or spawned
+by `bench.py --gpus N` itself (spawn_ranks: N fresh rank processes, rendezvous on 127.0.0.1);
+GOPs sharded by rank, no data-path collective; RCCL is used only after timing (max-time
+all_reduce, per-rank stats all_gather, bitstreams gathered to rank 0).
 
-The CPU leg (rank 0, N=1; --cpu-baseline quick|full|none) times the oracle on the host cores and
-reports BASELINE.md §3's parity block from the same frame: symbol / index mismatch counts,
-dPSNR, dbpp_est and a byte-exact stream check against the C oracle coder.
+After timing, every rank checks its own first GOP's frame 1 against the oracle (BASELINE.md §3's
+parity block: symbol / index mismatch counts, dPSNR, dbpp_est and a byte-exact stream check
+against the C oracle coder), gathered to rank 0 as `quality.parity_by_rank`; rank 0 then times
+the oracle on the host cores (--cpu-baseline quick|full|none) at every N, so every line, single-
+or multi-GPU, carries its own CPU baseline and parity.
 """
 from __future__ import annotations
 
@@ -113,16 +116,16 @@ def _median_time(fn, reps):
     return statistics.median(ts), ts
 
 
-def cpu_baseline(model, dev, frames_np, mode="quick"):
+def cpu_baseline(frames_np, mode="quick", coder=None):
     """The oracle (CPU PyTorch restatement of the reference forward, pinned to the reference's
-    golden fixtures) + the C oracle coder on the host cores, and the parity block of the same
-    frame (GOP 0, frame 1 coded against frame 0, which the GPU run also codes first).
+    golden fixtures) on the host cores, on GOP 0's frame 1 coded against frame 0 (the frame the GPU
+    run also codes first, and rank 0's parity frame). `coder`: the C oracle coder's symbols/s from
+    the parity block (one core).
 
     full (default; ~3 min of CPU work): 256x256 forward median of 3 after a warm-up at
     all cores and at 1 thread; 1080p encode+decode median of 3 after a warm-up at all cores, and once
-    at 1 thread (skipped, and said so, if predicted over ONE_THREAD_1080_BUDGET_S); C coder on one core.
-    quick (~30 s): 1080p once at all cores (the parity sample) instead of the 1080p protocol."""
-    from oracle import coder_ref as R
+    at 1 thread (skipped, and said so in seconds_1080_1thread_note, if predicted over
+    ONE_THREAD_1080_BUDGET_S). quick (~30 s): 1080p once at all cores instead of the 1080p protocol."""
     from oracle import dvc_ref
     from fastvideocodec_amd.synthetic import make_gop
     from fastvideocodec_amd.weights import seeded_torch_state_dict
@@ -133,12 +136,10 @@ def cpu_baseline(model, dev, frames_np, mode="quick"):
     cur = torch.from_numpy(frames_np[1:2].copy())
     ref = torch.from_numpy(frames_np[0:1].copy())
     Hp, Wp = cur.shape[-2:]
-    state = {}
 
     def enc_dec():
         out, inter = dvc_ref.forward(sd, cur, ref, return_intermediates=True)
         dvc_ref.decode(sd, ref, inter["quant_mv"], inter["compressed_z"], inter["compressed_feature"])
-        state["out"], state["inter"] = out, inter
 
     hb = _Heartbeat()
     with hb:
@@ -171,9 +172,6 @@ def cpu_baseline(model, dev, frames_np, mode="quick"):
                 torch.set_num_threads(cores)
             else:
                 one_thread_note = f"skipped: predicted {est:.0f} s > {ONE_THREAD_1080_BUDGET_S:.0f} s budget"
-        hb.stage = "parity block"
-
-        parity, coder = parity_block(model, dev, cur, ref, state["out"], state["inter"], R)
     cpu_model = ""
     try:
         cpu_model = next(l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name"))
@@ -188,11 +186,161 @@ def cpu_baseline(model, dev, frames_np, mode="quick"):
            "forward_256x256_s": {"threads": cores, "median_of_3": round(t_256, 4)},
            "forward_256x256_1thread_s": round(t_256_1, 4),
            "coder_1core": coder}
-    if one_thread_1080 is not None:
-        res["seconds_1080_1thread"] = round(one_thread_1080, 2)
+    res["seconds_1080_1thread"] = round(one_thread_1080, 2) if one_thread_1080 is not None else None
     if one_thread_note:
-        res["seconds_1080_1thread"] = one_thread_note
-    return res, parity
+        res["seconds_1080_1thread_note"] = one_thread_note
+    return res
+
+
+def dry_cpu_baseline():
+    """--dry-run stand-in for the CPU leg (no GPU anywhere): the oracle forward on one 64x64 frame
+    pair on the host cores, so the multi-rank result line carries the field it would carry."""
+    from oracle import dvc_ref
+    from fastvideocodec_amd.synthetic import make_gop
+    from fastvideocodec_amd.weights import seeded_torch_state_dict
+    cores = cpu_cores()
+    torch.set_num_threads(cores)
+    sd = seeded_torch_state_dict()
+    g = make_gop(64, 64, 2, 7)
+    c1, r1 = torch.from_numpy(g[1:2].copy()), torch.from_numpy(g[0:1].copy())
+    t = _median_time(lambda: dvc_ref.forward(sd, c1, r1), 1)[0]
+    return {"value": round(1.0 / t, 4), "unit": "P-frames/s", "cores": cores, "kind": "port", "mode": "dry-run",
+            "sample": f"dry run: 1 P-frame 64x64 oracle forward on {cores} threads = {t:.3f} s"}
+
+
+def rank_parity(model, dev, frames_np, unit, threads):
+    """BASELINE.md §3's parity block of this rank's first GOP (or view) `unit`: its frame 1 coded
+    against frame 0 by the oracle on `threads` host threads and by the GPU path (not timed)."""
+    from oracle import coder_ref as R
+    from oracle import dvc_ref
+    from fastvideocodec_amd.weights import seeded_torch_state_dict
+    old = torch.get_num_threads()
+    torch.set_num_threads(max(1, threads))
+    try:
+        cur = torch.from_numpy(frames_np[1:2].copy())
+        ref = torch.from_numpy(frames_np[0:1].copy())
+        out, inter = dvc_ref.forward(seeded_torch_state_dict(), cur, ref, return_intermediates=True)
+        par, coder = parity_block(model, dev, cur, ref, out, inter, R)
+    finally:
+        torch.set_num_threads(old)
+    par["frame"] = f"unit {unit} frame 1 vs frame 0"
+    return par, coder
+
+
+# ------------------------------------------------------------------ reference-comparable figures
+def reference_metrics(model, frames, reps=5):
+    """The figures the reference publishes for this path, measured here at
+    batch 1 on one GOP of this run's workload (frames: [T, 3, H, W] device tensor), after the timed
+    region. Secondary fields beside the headline:
+    * stage split (plot_hermes.py:547-554: SpyNet ME / MC / MV codec / residual codec): HIP
+      events on the launching stream around each stage of one encoder forward, median of `reps`;
+    * per-frame decode time (plot_hermes.py:735-737, simulation.py:133-137): the P-frames of the
+      GOP range-coded first, then each decoded (rANS decode -> hyperprior -> MV synthesis -> MC ->
+      residual synthesis) against the previous decoded frame with a host sync per frame;
+    * the drop-in path: models.parallel_compression (the reference's eval loop, models.py:368-383:
+      forward + bits estimate per P-frame at batch 1, the result of each frame feeding the next),
+      end to end including its host waits (the per-frame overflow probe, net.py:_run_checked)."""
+    from fastvideocodec_amd import kernels as K
+    from fastvideocodec_amd.models import parallel_compression
+
+    ev = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
+    T = frames.shape[0]
+    cur, ref = frames[1:2].contiguous(), frames[0:1].contiguous()
+    names = ("me_spynet", "mv_codec", "mc", "residual_codec", "rans_encode")
+    stages = {n: [] for n in names}
+    with torch.no_grad():
+        for _ in range(reps + 1):
+            e = [ev() for _ in range(len(names) + 1)]
+            e[0].record()
+            cur4 = K.nchw_to_nhwc(cur.float(), 4)
+            ref4 = K.nchw_to_nhwc(ref.float(), 4)
+            estmv = model.opticFlow.run(cur4, ref4)
+            e[1].record()
+            mvfeature = model.mvEncoder.run(estmv)
+            mv_up = model.mvDecoder.run(mvfeature)
+            e[2].record()
+            prediction, _ = model.motioncompensation(ref4, mv_up)
+            e[3].record()
+            feature = model.resEncoder.run(K.sub(cur4, prediction))
+            z = model.respriorEncoder.run(feature)
+            sigma = model.respriorDecoder.run(z)
+            model.resDecoder.run(feature, prediction)
+            e[4].record()
+            model.compress_tensors({"mvfeature": mvfeature, "z": z, "feature": feature, "sigma": sigma})
+            e[5].record()
+            torch.cuda.synchronize()
+            for i, n in enumerate(names):
+                stages[n].append(e[i].elapsed_time(e[i + 1]))
+    split = {n: round(statistics.median(v[1:]), 3) for n, v in stages.items()}
+
+    # per-frame decode at batch 1: encode the GOP's P-frames first (the encoder's own chain)
+    bss, x = [], frames[0:1]
+    with torch.no_grad():
+        for t in range(1, T):
+            bs, x = model.compress(frames[t:t + 1], x)
+            bss.append(bs)
+        torch.cuda.synchronize()
+        dec_ms, x = [], frames[0:1]
+        for _ in range(2):  # a warm pass, then the timed one
+            dec_ms, x = [], frames[0:1]
+            for bs in bss:
+                t0 = time.perf_counter()
+                x = model.decompress(bs, x)
+                torch.cuda.synchronize()
+                dec_ms.append((time.perf_counter() - t0) * 1e3)
+        enc_ms, x = [], frames[0:1]
+        for t in range(1, T):
+            t0 = time.perf_counter()
+            _, x = model.compress(frames[t:t + 1], x)
+            torch.cuda.synchronize()
+            enc_ms.append((time.perf_counter() - t0) * 1e3)
+
+    # the drop-in eval path (reference semantics: bits estimated, not coded)
+    data = frames.clone()
+    parallel_compression(None, model, data.clone(), False)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    parallel_compression(None, model, data, False)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    H, W = frames.shape[-2:]
+    return {
+        "resolution": f"{W}x{H}", "batch": 1,
+        "stage_ms_b1": split,
+        "stage_note": "one encoder forward at batch 1 on one stream, HIP events between stages (median of "
+                      f"{reps}); reference (BASELINE.md §1, plot_hermes.py:547-554, trained weights, NVIDIA, "
+                      "resolution not recorded): ME / MC / MV codec / residual codec = 14.3 / 6.6 / 9.8 / 2.4 ms "
+                      "(GTX 1080 Ti), 9.2 / 4.0 / 3.7 / 1.6 ms (RTX 2080 Ti); their MV / residual codec "
+                      "excludes range coding (estimated bits), reported here separately as rans_encode",
+        "decode_ms_per_frame_b1": {"median": round(statistics.median(dec_ms), 3), "min": round(min(dec_ms), 3),
+                                   "frames": len(dec_ms)},
+        "decode_fps_b1": round(1e3 / statistics.median(dec_ms), 2),
+        "decode_note": "bitstream -> rANS decode -> hyperprior -> MV synthesis -> MC -> residual synthesis per "
+                       "P-frame, host sync per frame; reference per-frame decode time 38.2 / 28.0 / 10.0 ms on "
+                       "GTX 1080 Ti / RTX 2080 Ti / RTX 3090 Ti (plot_hermes.py:735-737, simulation.py:133-137)",
+        "encode_ms_per_frame_b1": {"median": round(statistics.median(enc_ms), 3), "frames": len(enc_ms)},
+        "dropin_parallel_compression": {"pframes_per_s": round((T - 1) / dt, 2), "seconds": round(dt, 4),
+                                        "pframes": T - 1,
+                                        "note": "models.parallel_compression on one GOP at batch 1 (forward + "
+                                                "bits estimate, each frame's recon feeding the next), including "
+                                                "the per-frame host wait of the overflow probe (net.py:_run_checked)"},
+    }
+
+
+# per-rank parity summary gathered to rank 0 (fixed order of floats)
+PARITY_FIELDS = ("checked", "symbols", "symbol_mismatches", "index_mismatches", "dpsnr_db", "dbpp_est_rel",
+                 "streams", "streams_t1_equal", "streams_equal_on_oracle_symbols")
+
+
+def parity_vector(par):
+    if par is None:
+        return [0.0] * len(PARITY_FIELDS)
+    lat = par["latents"].values()
+    return [1.0, float(sum(v["symbols"] for v in lat)), float(sum(v["symbol_mismatches"] for v in lat)),
+            float(sum(v["index_mismatches"] for v in lat)), float(par["dpsnr_db"]), float(par["dbpp_est_rel"]),
+            float(sum(v["streams"] for v in lat)),
+            float(sum(v["streams_bytes_equal_c_oracle_same_symbols"] for v in lat)),
+            float(sum(v["streams_bytes_equal_c_oracle_on_oracle_symbols"] for v in lat))]
 
 
 def parity_block(model, dev, cur, ref, oracle_out, inter, R):
@@ -324,6 +472,10 @@ class GpuGopJob:
                 print(f"{k:40s} n={n:5d} ms={ms:9.2f} TF/s={fl / (ms * 1e-3) / 1e12:7.2f}", file=sys.stderr)
         return r
 
+    def parity(self, threads):
+        """Parity block of this rank's first unit, frame 1 (rank_parity)."""
+        return rank_parity(self.model, self.dev, self.gops_np[0], self.shard[0], threads)
+
     def verify(self):
         from fastvideocodec_amd.gop import encode_decode_gop
         overflow_before = getattr(self.model, "overflow_events", 0)
@@ -372,6 +524,15 @@ class HostRehearsalJob:
     def after_timing(self):
         return None
 
+    def parity(self, threads):
+        """Stand-in parity block (no GPU): the fields a real rank reports, all zero mismatches."""
+        lat = {"mv": (128, 2), "z": (64, 0), "feature": (96, 0)}
+        par = {"frame": f"unit {self.shard[0]} frame 1 vs frame 0 (dry run)", "dpsnr_db": 0.0, "dbpp_est_rel": 0.0,
+               "latents": {k: {"symbols": c * 100, "symbol_mismatches": 0, "index_mismatches": 0, "streams": c,
+                               "streams_bytes_equal_c_oracle_same_symbols": c,
+                               "streams_bytes_equal_c_oracle_on_oracle_symbols": c} for k, (c, _) in lat.items()}}
+        return par, None
+
     def verify(self):
         payload = b"".join(bytes([u % 256]) * (100 + u) for u in self.shard)
         return {"bitexact": True, "nbytes": len(payload), "psnr": 30.0, "payload": payload,
@@ -398,6 +559,12 @@ def run_rank(job, args, rank, world, device):
 
     prof = job.after_timing()
     ver = job.verify()
+    # every rank checks its own first unit against the oracle (host threads shared among the
+    # node's ranks), before the collectives so the ranks do it concurrently
+    par = coder = None
+    if getattr(args, "cpu_baseline", "none") != "none" and hasattr(job, "parity"):
+        par, coder = job.parity(max(1, cpu_cores() // world))
+    pvec = fdist.gather_stats(parity_vector(par), device)
     dt_max = fdist.max_over_ranks(dt, device)
     allst = fdist.gather_stats([1.0 if ver["bitexact"] else 0.0, float(ver["nbytes"]), ver["psnr"],
                                 float(job.units), float(ver["overflow_recomputes"])], device)
@@ -412,6 +579,14 @@ def run_rank(job, args, rank, world, device):
     bytes_all = float(allst[:, 1].sum())
     enc_tf, dec_tf = tflop_per_pframe(job.Hp, job.Wp)
     res_label = f"{args.width}x{args.height} (padded {job.Wp}x{job.Hp})"
+    tree_info = None
+    if getattr(args, "tree", False):
+        from fastvideocodec_amd.tree_gop import coding_layers
+        lay = coding_layers(args.gop - 1, extend=True)
+        tree_info = {"layers": [[t for t, _ in l] for l in lay], "depth": len(lay),
+                     "structure": ("the reference's graph_from_batch tree (models.py:683-728)" if args.gop - 1 <= 30
+                                   else "EXTENSION (not a reference structure): prefix of the 62-frame binary tree "
+                                        "(binary_tree_graph), the reference's graphs stop at 30 P-frames")}
     result = {
         "metric": metric_name(args.height, args.width),
         "value": round(value, 3),
@@ -429,7 +604,8 @@ def run_rank(job, args, rank, world, device):
                                 f"{' as an LSVC reference tree (models.py:683-728), one batch per tree layer' if args.tree else ''}"
                                 f", lambda=1024 slot",
                     "gops_per_gpu": job.units, "frames_counted": "P-frames only (I-frame pass-through)",
-                    "parallelism": f"gop-shard x{world}"} if args.views <= 0 else
+                    "parallelism": f"gop-shard x{world}", **({"tree": tree_info} if tree_info else {})}
+                   if args.views <= 0 else
                    {"workload": f"{args.views}-view DVC P-frame encode+decode with rANS, {res_label} GOP-{args.gop} "
                                 f"per view, lambda=1024 slot",
                     "views": args.views, "views_per_gpu": job.units,
@@ -449,6 +625,32 @@ def run_rank(job, args, rank, world, device):
                             "figures; the coder's symbol statistics (and so its timing) are those of untrained "
                             "weights (~5 bpp vs DVC's 0.137 bpp at lambda=1024)"},
     }
+    if par is not None:
+        by_rank = []
+        for r, v in enumerate(pvec):
+            d = dict(zip(PARITY_FIELDS, (float(x) for x in v)))
+            if not d["checked"]:
+                by_rank.append({"rank": r, "checked": False})
+                continue
+            by_rank.append({"rank": r, "unit": result["shards"]["by_rank"][r][0],
+                            "symbol_mismatch_rate": d["symbol_mismatches"] / max(d["symbols"], 1.0),
+                            "symbol_mismatches": int(d["symbol_mismatches"]), "symbols": int(d["symbols"]),
+                            "index_mismatches": int(d["index_mismatches"]), "dpsnr_db": d["dpsnr_db"],
+                            "dbpp_est_rel": d["dbpp_est_rel"],
+                            "bitstream_t1_byte_exact": d["streams_t1_equal"] == d["streams"],
+                            "streams_bytes_equal_on_oracle_symbols": int(d["streams_equal_on_oracle_symbols"]),
+                            "streams": int(d["streams"])})
+        checked = [b for b in by_rank if b.get("checked", True)]
+        result["quality"]["parity"] = par  # rank 0's full block
+        result["quality"]["parity_by_rank"] = by_rank
+        result["quality"]["parity_all_ranks"] = {
+            "ranks_checked": len(checked),
+            "max_symbol_mismatch_rate": max(b["symbol_mismatch_rate"] for b in checked),
+            "symbol_mismatch_bound": 1.56e-5,
+            "max_dpsnr_db": max(b["dpsnr_db"] for b in checked), "dpsnr_bound_db": 1e-4,
+            "bitstream_t1_byte_exact": all(b["bitstream_t1_byte_exact"] for b in checked)}
+        if coder is not None:
+            result["_coder"] = coder
     if prof is not None:
         result.update(roofline_fields(prof, job, args))
     return result
@@ -556,6 +758,9 @@ def parse_args(argv=None):
                     help="CPU leg + parity block on rank 0 at N=1: full (default; BASELINE.md §3 protocol, "
                          "~3 min), quick (~30 s), none")
     ap.add_argument("--no-cpu-baseline", action="store_true", help="same as --cpu-baseline none")
+    ap.add_argument("--no-ref-metrics", dest="ref_metrics", action="store_false",
+                    help="skip the reference-comparable batch-1 figures (stage split, per-frame decode time, "
+                         "drop-in parallel_compression throughput) rank 0 measures after timing")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--breakdown", action="store_true", help="print per-conv-geometry timing to stderr")
     ap.add_argument("--tree", action="store_true",
@@ -595,17 +800,33 @@ def spawn_ranks(n, argv):
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
     rc = 0
     live = list(procs)
-    while live:
-        for p in list(live):
-            code = p.poll()
-            if code is None:
-                continue
-            live.remove(p)
-            if code != 0 and rc == 0:
-                rc = code
-                for q in live:
+    try:
+        while live:
+            for p in list(live):
+                code = p.poll()
+                if code is None:
+                    continue
+                live.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code
+                    for q in live:
+                        q.terminate()
+            time.sleep(0.05)
+    finally:
+        # interrupted (KeyboardInterrupt / SIGTERM turned into an exception): stop the exact rank
+        # processes this parent started, then kill what is still alive, and report a failure
+        if live:
+            rc = rc or 1
+            for q in live:
+                if q.poll() is None:
                     q.terminate()
-        time.sleep(0.05)
+            deadline = time.time() + 10
+            for q in live:
+                try:
+                    q.wait(timeout=max(0.1, deadline - time.time()))
+                except subprocess.TimeoutExpired:
+                    q.kill()
+                    q.wait()
     return rc
 
 
@@ -635,10 +856,16 @@ def main(argv=None):
     result = run_rank(job, args, rank, world, dev)
     if args.dry_run and rank == 0:
         result["data"] = "dry run: host rehearsal job, no GPU work (launcher / sharding / collectives only)"
-    if rank == 0 and world == 1 and args.cpu_baseline != "none" and not args.dry_run:
-        cb, parity = cpu_baseline(job.model, dev, job.gops_np[0], args.cpu_baseline)
-        result["cpu_baseline"] = cb
-        result["quality"]["parity"] = parity
+    if rank == 0 and not args.dry_run and args.ref_metrics:
+        result["reference_comparable"] = reference_metrics(job.model, job.frames[0])
+    # the CPU leg on rank 0 at every N, after the timed region and the collectives
+    if rank == 0 and args.cpu_baseline != "none":
+        coder = result.pop("_coder", None)
+        if args.dry_run:
+            result["cpu_baseline"] = dry_cpu_baseline()
+        else:
+            result["cpu_baseline"] = cpu_baseline(job.gops_np[0], args.cpu_baseline, coder)
+        result["cpu_baseline"]["n_gpus_in_run"] = world
     if rank == 0:
         line = json.dumps(result)
         print(line, flush=True)

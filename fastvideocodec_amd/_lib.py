@@ -27,6 +27,7 @@ _SIGS = {
     "fvc_conv_x3_supported": (c_int, [c_int] * 5),
     "fvc_deconv_x3_all_classes": (c_int, [c_int] * 4),
     "fvc_conv_x3_wpack_bytes": (c_size_t, [c_int] * 5),
+    "fvc_conv_x3_layout_id": (ctypes.c_uint, [c_int] * 5),
     "fvc_conv_x3_pack_weight": (c_int, [vp, vp, vp] + [c_int] * 5),
     "fvc_conv2d_nhwc_x3": (c_int, [vp, vp, c_float, vp, vp, vp] + [c_int] * 11 + [vp, vp, c_int, vp]),
     "fvc_deconv2d_nhwc_x3": (c_int, [vp, vp, c_float, vp, vp, vp] + [c_int] * 11 + [vp, vp, c_int, vp]),

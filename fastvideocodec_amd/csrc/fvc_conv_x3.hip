@@ -1409,6 +1409,36 @@ int fvc_deconv_x3_all_classes(int cin, int cout, int ksize, int stride) {
   return x3_cfg(cin, cout, ksize, stride, 1, c) && c.dx ? 1 : 0;
 }
 
+// The pack layout the current configuration gives this geometry (a hash of every X3Cfg field the
+// pack's fragment order depends on: kernel family, channel chunk, pair-tap form, taps and k-steps
+// per class, total size), or 0 when the x3 path does not take the layer. The env switches that
+// choose these (FVC_DX, FVC_X3_PT, FVC_X3_CIN4, FVC_X3_CC, FVC_X3_SMALLN) are read at pack AND at
+// launch: callers record the id with a pack and compare it before each launch, so a switch
+// flipped in between is refused instead of running on a pack of another layout.
+unsigned fvc_conv_x3_layout_id(int cin, int cout, int ksize, int stride, int transposed) {
+  X3Cfg c;
+  if (!x3_cfg(cin, cout, ksize, stride, transposed, c)) return 0u;
+  unsigned h = 2166136261u;
+  auto mix = [&](long long v) {
+    for (int i = 0; i < 8; ++i) {
+      h ^= (unsigned)(v >> (8 * i)) & 0xffu;
+      h *= 16777619u;
+    }
+  };
+  mix(c.dx);
+  mix(c.cc);
+  mix(c.pt);
+  mix(c.nchunks);
+  mix(c.ntp);
+  mix(c.nclass);
+  for (int cl = 0; cl < c.nclass; ++cl) {
+    mix(c.ntaps[cl]);
+    mix(c.nks[cl]);
+  }
+  mix(c.wtotal);
+  return h ? h : 1u;
+}
+
 size_t fvc_conv_x3_wpack_bytes(int cin, int cout, int ksize, int stride, int transposed) {
   X3Cfg c;
   if (!x3_cfg(cin, cout, ksize, stride, transposed, c)) return 0;

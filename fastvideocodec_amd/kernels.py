@@ -327,6 +327,7 @@ class PackedConv:
             _lib.call("fvc_conv_x3_pack_weight", w.data_ptr(), packed.data_ptr(), ctypes.addressof(osc), cin, cout,
                       ksize, stride, int(transposed))
             self.osc = float(osc.value)
+            self.layout = int(lib.fvc_conv_x3_layout_id(cin, cout, ksize, stride, int(transposed)))
         else:
             n = lib.fvc_conv_wpack_floats(cin, cout, ksize, stride, int(transposed))
             if n == 0:
@@ -336,6 +337,15 @@ class PackedConv:
                       int(transposed))
         self.wpack = packed.to(device)
         self.bias = bias.detach().to(device, torch.float32).contiguous()
+
+    def _check_layout(self):
+        """The pack's layout must be the one the launch will assume: FVC_DX / FVC_X3_PT / FVC_X3_CIN4 /
+        FVC_X3_CC / FVC_X3_SMALLN are read by the C side at pack and at launch."""
+        now = int(_lib.load().fvc_conv_x3_layout_id(self.cin, self.cout, self.ksize, self.stride,
+                                                      int(self.transposed)))
+        if now != self.layout:
+            raise _lib.FvcError("x3 weight pack was built under another layout configuration (an FVC_DX / "
+                                "FVC_X3_* switch changed since packing); re-create the PackedConv")
 
     def out_hw(self, h, w):
         if self.transposed:
@@ -385,6 +395,7 @@ class PackedConv:
                       stream_handle())
             wino = True
         elif self.x3:
+            self._check_layout()
             fn = "fvc_deconv2d_nhwc_x3" if self.transposed else "fvc_conv2d_nhwc_x3"
             _lib.call(fn, x.data_ptr(), self.wpack.data_ptr(), self.osc, self.bias.data_ptr(), _ptr(res),
                       y.data_ptr(), B, H, W, self.cin, self.cout, self.ksize, self.stride, in_op, act, post,
@@ -437,6 +448,7 @@ class PackedConv:
                       overflow_flag(x.device).data_ptr(), sched_scratch(x.device).data_ptr(), SCHED_LEN,
                       stream_handle())
         else:
+            self._check_layout()
             _lib.call("fvc_conv2d_nhwc_x3_pool", x.data_ptr(), self.wpack.data_ptr(), self.osc, self.bias.data_ptr(),
                       _ptr(res), y.data_ptr(), pool.data_ptr(), B, H, W, self.cin, self.cout, self.ksize, act,
                       _STATE["cu_reserve"], overflow_flag(x.device).data_ptr(), sched_scratch(x.device).data_ptr(),
@@ -492,6 +504,7 @@ class PackedConv:
                       _STATE["cu_reserve"], overflow_flag(x.device).data_ptr(), sched_scratch(x.device).data_ptr(),
                       SCHED_LEN, stream_handle())
         else:
+            self._check_layout()
             fn = "fvc_deconv2d_nhwc_x3_tap" if self.transposed else "fvc_conv2d_nhwc_x3_tap"
             _lib.call(fn, x.data_ptr(), self.wpack.data_ptr(), self.osc, self.bias.data_ptr(), _ptr(res), P.data_ptr(),
                       B, H, W, self.cin, self.cout, self.ksize, self.stride, act, tap.wpack.data_ptr(), tap.osc,

@@ -94,6 +94,11 @@ int fvc_deconv2d_nhwc_f32(const float* x, const float* wpack, const float* bias,
  * the persistent grid walks a fixed run. */
 int fvc_conv_x3_supported(int cin, int cout, int ksize, int stride, int transposed);
 size_t fvc_conv_x3_wpack_bytes(int cin, int cout, int ksize, int stride, int transposed);
+/* Layout id (nonzero) of the pack fvc_conv_x3_pack_weight writes for this geometry under the
+ * current configuration, 0 if the x3 path does not take it. The FVC_DX / FVC_X3_PT / FVC_X3_CIN4 /
+ * FVC_X3_CC / FVC_X3_SMALLN switches are read at pack and at launch time: record the id with the
+ * pack and compare before launching (the Python layer refuses a mismatch). */
+unsigned fvc_conv_x3_layout_id(int cin, int cout, int ksize, int stride, int transposed);
 int fvc_conv_x3_pack_weight(const float* w_host, void* wpack_host, float* osc_out, int cin,
                             int cout, int ksize, int stride, int transposed);
 int fvc_conv2d_nhwc_x3(const float* x, const void* wpack, float osc, const float* bias,

@@ -199,3 +199,27 @@ def test_x3_dispatch_count_mirrors_the_batch_split(monkeypatch):
     monkeypatch.setenv("FVC_X3_SPLIT_BYTES", "1000")
     assert x3_dispatches(5, 300) == 2             # 1500 B -> 2 + 3 images (600, 900 B): two launches
     assert x3_dispatches(8, 300) == 4             # 2400 -> 4 + 4 (1200 each) -> 2 + 2 + 2 + 2
+
+
+def test_x3_layout_id_tracks_layout_switches(monkeypatch):
+    """the env switches that change an x3 pack's layout change its layout id (which
+    PackedConv records at pack time and compares before every launch); other knobs do not."""
+    lib = _lib.load()
+    for k in ("FVC_DX", "FVC_X3_PT", "FVC_X3_CC", "FVC_X3_CIN4", "FVC_X3_SMALLN", "FVC_X3_WM"):
+        monkeypatch.delenv(k, raising=False)
+    dx = lib.fvc_conv_x3_layout_id(128, 128, 3, 2, 1)
+    pt = lib.fvc_conv_x3_layout_id(32, 16, 7, 1, 0)
+    c4 = lib.fvc_conv_x3_layout_id(3, 64, 5, 2, 0)
+    wide = lib.fvc_conv_x3_layout_id(64, 64, 3, 1, 0)
+    assert 0 not in (dx, pt, c4, wide)
+    assert lib.fvc_conv_x3_layout_id(8, 160, 3, 1, 0) == 0  # not an x3 geometry
+    monkeypatch.setenv("FVC_X3_WM", "1")  # block shape only: same pack
+    assert lib.fvc_conv_x3_layout_id(64, 64, 3, 1, 0) == wide
+    monkeypatch.setenv("FVC_DX", "0")
+    assert lib.fvc_conv_x3_layout_id(128, 128, 3, 2, 1) not in (0, dx)
+    monkeypatch.setenv("FVC_X3_PT", "0")
+    assert lib.fvc_conv_x3_layout_id(32, 16, 7, 1, 0) not in (0, pt)
+    monkeypatch.setenv("FVC_X3_CC", "8")
+    assert lib.fvc_conv_x3_layout_id(64, 64, 3, 1, 0) not in (0, wide)
+    monkeypatch.setenv("FVC_X3_CIN4", "0")
+    assert lib.fvc_conv_x3_layout_id(3, 64, 5, 2, 0) == 0  # back on the fp32 kernels

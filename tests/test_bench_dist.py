@@ -109,6 +109,15 @@ def test_bench_gpus2_spawns_two_ranks(tmp_path):
     assert res["quality"]["bitstreams_gathered_to_rank0_bytes"] == sum(100 + g for g in range(6))
     dt = 2 * 6 * 3 / res["value"]                   # 6 GOPs x 3 P-frames per step
     assert dt >= 2 * 0.010 * 0.9                    # rank 1's 10 ms steps bound the time
+    # a multi-GPU line carries its own CPU baseline (rank 0, after timing) and every
+    # rank's parity block, gathered to rank 0
+    cb = res["cpu_baseline"]
+    assert cb["n_gpus_in_run"] == 2 and cb["value"] > 0 and cb["cores"] >= 1
+    pr = res["quality"]["parity_by_rank"]
+    assert [p["rank"] for p in pr] == [0, 1] and [p["unit"] for p in pr] == [0, 1]
+    assert all(p["bitstream_t1_byte_exact"] and p["symbols"] == 28800 for p in pr)
+    assert res["quality"]["parity_all_ranks"]["ranks_checked"] == 2
+    assert res["quality"]["parity"]["frame"].startswith("unit 0 ")
 
 
 def test_bench_gpus4_gop32_one_gop_per_rank(tmp_path):
@@ -139,3 +148,21 @@ def test_bench_refuses_gpus_mismatch_under_launcher(monkeypatch):
     monkeypatch.setenv("RANK", "0")
     with pytest.raises(SystemExit, match="--gpus 2 != WORLD_SIZE 1"):
         bench.main(["--gpus", "2", "--dry-run"])
+
+
+def test_bench_no_cpu_baseline_omits_parity(tmp_path):
+    """--cpu-baseline none: no CPU leg and no parity at any N."""
+    res = _run_bench_cli(["--gpus", "2", "--steps", "1", "--warmup", "0", "--gops-per-gpu", "1", "--height", "64",
+                          "--width", "128", "--gop", "3", "--cpu-baseline", "none"], tmp_path)
+    assert "cpu_baseline" not in res and "parity_by_rank" not in res["quality"]
+
+
+def test_bench_tree_labels_extension(tmp_path):
+    """a tree run past the reference's 30-frame graphs says so in its config block."""
+    res = _run_bench_cli(["--tree", "--gop", "32", "--gops-per-gpu", "1", "--steps", "1", "--warmup", "0",
+                          "--height", "64", "--width", "128", "--cpu-baseline", "none"], tmp_path)
+    tr = res["config"]["tree"]
+    assert tr["structure"].startswith("EXTENSION") and sum(len(l) for l in tr["layers"]) == 31
+    res = _run_bench_cli(["--tree", "--gop", "12", "--gops-per-gpu", "1", "--steps", "1", "--warmup", "0",
+                          "--height", "64", "--width", "128", "--cpu-baseline", "none"], tmp_path)
+    assert res["config"]["tree"]["layers"] == [[1, 8], [2, 5, 9], [3, 4, 6, 7, 10, 11]]

@@ -137,6 +137,55 @@ def test_views8_1080p_config4(dev):
     assert dpsnr <= 1e-4, dpsnr
 
 
+@pytest.mark.timeout(420)
+def test_4k_gop32_one_rank_share(dev):
+    """BASELINE configs[3] at its own workload: one rank's share of the 4-GPU split, i.e. one
+    3840x2160 (padded to 2176) GOP-32 = 31 chained P-frames through the bench's rank job
+    (models.py:372-376's sequential loop, encode + rANS + decode). Checks: decoder recon == encoder
+    recon bit for bit over all 31 P-frames, no split-precision overflow anywhere in the chain (31
+    chained reconstructions at 4K, flag clear after frame 31), and frame 1's latents / PSNR vs the
+    CPU oracle at the 1080p T3 bounds (aggregate flips <= 1.56e-5, dPSNR <= 1e-4 dB)."""
+    import os
+
+    import bench
+    from fastvideocodec_amd import kernels as K
+    from fastvideocodec_amd.gop import encode_decode_gop
+    from fastvideocodec_amd.weights import seeded_torch_state_dict
+    from oracle import dvc_ref
+
+    job = bench.GpuGopJob(_args(gop=32, gops_per_gpu=1, height=2160, width=3840), 2, 4, dev)
+    assert job.units == 1 and job.shard == [2] and tuple(job.frames.shape) == (1, 32, 3, 2176, 3840)
+    K.x3_overflow(reset=True)
+    bss, dec, _, enc = encode_decode_gop(job.model, job.frames, check=True, overlap=True)
+    torch.cuda.synchronize()
+    assert len(dec) == 31 and len(bss) == 31
+    for t, (a, b) in enumerate(zip(dec, enc), 1):
+        assert torch.equal(a, b), f"P-frame {t}: decoder recon != encoder recon"
+    assert getattr(job.model, "overflow_events", 0) == 0
+    assert not K.x3_overflow(reset=True)
+    assert all(bs.precision == "x3" for bs in bss)
+    del dec, enc, bss
+
+    out, t = job.model(job.frames[:, 1].contiguous(), job.frames[:, 0].contiguous(), return_intermediates=True)
+    torch.cuda.synchronize()
+    cur, ref = job.frames[0:1, 1].cpu(), job.frames[0:1, 0].cpu()
+    torch.set_num_threads(min(16, len(os.sched_getaffinity(0))))
+    (o_clip, o_mse, *_), inter = dvc_ref.forward(seeded_torch_state_dict(), cur, ref, return_intermediates=True)
+    nflip = ntot = 0
+    for name, gname, c in (("mvfeature", "quant_mv", 128), ("feature", "compressed_feature", 96),
+                           ("z", "compressed_z", 64)):
+        got = np.round(t[name][..., :c].permute(0, 3, 1, 2).cpu().numpy())
+        d = got != inter[gname].numpy()
+        nflip += int(d.sum())
+        ntot += d.size
+    print(f"4K frame 1: {nflip} flips of {ntot} symbols")
+    assert nflip / ntot <= 1.56e-5, (nflip, ntot)
+    sse_gpu = float(((out[0].cpu() - cur) ** 2).sum())
+    sse_cpu = float(((o_clip - cur) ** 2).sum())
+    dpsnr = abs(10 * np.log10(sse_cpu / sse_gpu))
+    assert dpsnr <= 1e-4, dpsnr
+
+
 def test_gop32_four_rank_split(dev):
     """BASELINE configs[3]'s GOP structure (GOP-32: 31 P-frames per I-frame, one GOP per rank over
     4 ranks), at a small frame size, with the ranks' jobs run one after the other on this GPU: rank r

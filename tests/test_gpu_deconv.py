@@ -135,3 +135,22 @@ def test_deconv_all_classes_overflow_flag(dev, monkeypatch):
     x[0, 77, 4, 13] = 7e4
     pc(to_nhwc(x).to(dev))
     assert K.x3_overflow(reset=True)
+
+
+def test_pack_layout_switch_refused(dev, monkeypatch):
+    """an x3 pack launched after a layout switch flipped (FVC_DX here: the all-classes
+    pack has one full-channel chunk, the per-class pack 32-channel chunks) is refused instead of
+    running on a pack of another layout; flipping back makes it usable again."""
+    from fastvideocodec_amd import _lib
+    g = torch.Generator().manual_seed(11)
+    w = torch.randn(128, 128, 3, 3, generator=g) * 0.03
+    pc = _pack(w, torch.zeros(128), 3, dev, monkeypatch, True)
+    x = to_nhwc(torch.randn(1, 128, 8, 16, generator=g)).to(dev)
+    a = pc(x)
+    monkeypatch.setenv("FVC_DX", "0")
+    with pytest.raises(_lib.FvcError):
+        pc(x)
+    monkeypatch.setenv("FVC_DX", "1")
+    b = pc(x)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)

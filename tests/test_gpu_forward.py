@@ -105,8 +105,15 @@ def test_gop_chain_vs_golden(model, dev):
     x_hat, loss, img_loss, be_loss, _, psnr, psnr_list, aux, aux2, _, _ = parallel_compression(None, model, data, False)
     assert x_hat.shape == (3, 3, 256, 256)
     drift = np.abs(np.array(psnr_list) - exp_psnr)
-    print("closed-loop PSNR drift per frame (dB):", drift)
-    assert drift[0] <= TOL_PSNR_DB and drift.max() <= 2e-2, drift
+    # the closed-loop bound is anchored to the measured floor of the fp32-MFMA convs on the same
+    # chain (the split-precision path must not drift more than twice what plain fp32 does)
+    from fastvideocodec_amd import kernels as K
+    with K.precision("f32"):
+        psnr_f32 = parallel_compression(None, model, gop.clone(), False)[6]
+    drift_f32 = np.abs(np.array(psnr_f32) - exp_psnr)
+    print("closed-loop PSNR drift per frame (dB): x3", drift, "f32", drift_f32)
+    assert drift[0] <= TOL_PSNR_DB, drift
+    assert drift.max() <= max(2 * drift_f32.max(), 1e-4), (drift, drift_f32)
     exp_bpp = np.mean([float(g[f"f{i}_bpp"]) for i in range(1, 4)])
     assert abs(be_loss - exp_bpp) <= 1e-2 * exp_bpp
 

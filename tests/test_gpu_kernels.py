@@ -458,7 +458,8 @@ def test_gdn_x3_vs_fp32_and_float64(dev, shape, inverse, monkeypatch):
     """The split-precision GDN kernel (k_gdn_x3: norm on fp16 hi/lo MFMAs) against float64 torch
     (GDN.py:63-93) and against the fp32-MFMA kernel (FVC_GDN_X3=0) at ragged pixel counts (groups
     of 32 cut anywhere), with off-diagonal gamma entries 6 orders of magnitude below the diagonal;
-    a 5000-valued input sends its group down the fp32 chain inside the kernel with no flag."""
+    a 5000-valued input (x^2 = 2.5e7, past the fp16 range unscaled) is taken by the per-pixel
+    power-of-two scale with no flag."""
     B, H, W = shape
     g = torch.Generator().manual_seed(H * W + int(inverse))
     x = torch.randn(B, 64, H, W, generator=g) * 3
@@ -480,6 +481,33 @@ def test_gdn_x3_vs_fp32_and_float64(dev, shape, inverse, monkeypatch):
         e32 = float((outs["0"] - ref).abs().max())
         print(f"{shape} inv={inverse} big={xin is big}: x3 {e3 / scale:.2e}, fp32 {e32 / scale:.2e} of scale")
         assert e3 <= 1e-6 * scale and e3 <= 4 * e32 + 1e-7 * scale, (e3, e32, scale)
+
+
+@pytest.mark.parametrize("inverse", [False, True])
+def test_gdn_x3_small_activations_small_beta(dev, inverse, monkeypatch):
+    """small activations (|x| ~ 1e-2 .. 1e-4, so x^2 is far below the fp16 normal range
+    without a scale) with a small beta (1e-3 .. 1e-6, compressai's beta_min is 1e-6): the norm is
+    dominated by the gamma . x^2 term, and its relative error must stay at the split-precision
+    level (per-pixel power-of-two scale) -- compared elementwise against float64, relative to each
+    output value, not to the tensor's max."""
+    g = torch.Generator().manual_seed(1234 + int(inverse))
+    B, H, W = 2, 13, 37
+    x = torch.randn(B, 64, H, W, generator=g) * 1e-2
+    x[:, :, :, :9] *= 1e-2  # some pixels two orders of magnitude smaller still
+    beta = torch.rand(64, generator=g) * 1e-3 + 1e-6
+    gamma = torch.rand(64, 64, generator=g) * 0.05 + torch.eye(64) * 0.5
+    norm = torch.sqrt(F.conv2d(x.double() ** 2, gamma.double()[:, :, None, None], beta.double()))
+    ref = x.double() * norm if inverse else x.double() / norm
+    outs = {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("FVC_GDN_X3", flag)
+        outs[flag] = from_nhwc(K.gdn(to_nhwc(x).to(dev), beta.to(dev), gamma.to(dev).contiguous(),
+                                     inverse).cpu(), 64).double()
+    den = ref.abs() + 1e-30
+    r3 = float(((outs["1"] - ref).abs() / den).max())
+    r32 = float(((outs["0"] - ref).abs() / den).max())
+    print(f"small x, small beta, inv={inverse}: max relative error x3 {r3:.2e}, fp32 {r32:.2e}")
+    assert r3 <= 2e-6 and r3 <= 4 * r32 + 1e-7, (r3, r32)
 
 
 def test_gdn_x3_tap_form_vs_fp32_form(dev, monkeypatch):

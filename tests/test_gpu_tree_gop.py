@@ -90,11 +90,21 @@ def test_tree_gop_vs_oracle(model, dev, seeded_sd):
             assert flips <= 1e-3 * (128 * 8 * 12 + 96 * 8 * 12 + 64 * 2 * 3), (t, flips)
             # closed loop: the oracle's own tree
             rec_o[t] = dvc_ref.forward(seeded_sd, cur, rec_o[p])[0]
+    # closed-loop drift bound anchored to the fp32-MFMA convs' own drift on the same tree
+    from fastvideocodec_amd import kernels as K
+    with K.precision("f32"):
+        _, _, _, enc32 = encode_decode_tree_gop(model, frames, check=True)
+        torch.cuda.synchronize()
+    drift, drift32 = [], []
     for t in range(1, T):
         cur = fr[t:t + 1]
-        pd = 10 * np.log10(1 / float(((enc[t].cpu() - cur) ** 2).mean()))
         po = 10 * np.log10(1 / float(((rec_o[t] - cur) ** 2).mean()))
-        assert abs(pd - po) <= 5e-3, (t, pd, po)
+        pd = 10 * np.log10(1 / float(((enc[t].cpu() - cur) ** 2).mean()))
+        p32 = 10 * np.log10(1 / float(((enc32[t].cpu() - cur) ** 2).mean()))
+        drift.append(abs(pd - po))
+        drift32.append(abs(p32 - po))
+    print("tree closed-loop PSNR drift (dB): x3", np.array(drift), "f32", np.array(drift32))
+    assert max(drift) <= max(2 * max(drift32), 1e-4), (drift, drift32)
 
 
 def test_tree_gop_streaming_join_false(model, dev):
