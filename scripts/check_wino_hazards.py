@@ -1,6 +1,6 @@
 """Audit a hipcc -save-temps .s of fvc_conv_wino.hip for the MFMA-operand wait states the inline-asm
-blocks rely on: no VALU / v_accvgpr_write may write an MFMA source (A, B) within 2 wait states
-before it (cdna_hip_programming.md §5.7 item 2), and no non-MFMA instruction may read or write an
+blocks rely on (the MFMAs inside inline-asm strings; hipcc pads its own builtin MFMAs): no VALU /
+v_accvgpr_write may write an MFMA source (A, B) within 2 wait states before it (cdna_hip_programming.md §5.7 item 2), and no non-MFMA instruction may read or write an
 MFMA destination within 12 states after it unless an MFMA accumulate chain takes it. Counts one
 state per instruction and N+1 per s_nop N (a lower bound on the hardware's distance).
 
@@ -24,27 +24,35 @@ def regs(text):
 
 
 def parse(lines):
+    """(opcode, operands, text, inside an inline-asm block) per instruction."""
     ins = []
+    in_asm = False
     for l in lines:
+        if ";;#ASMSTART" in l:
+            in_asm = True
+        elif ";;#ASMEND" in l:
+            in_asm = False
         t = l.split(";")[0].strip()
         if not t or t.endswith(":") or t.startswith("."):
             continue
         op, _, rest = t.partition(" ")
         ops = [x.strip() for x in rest.split(",")] if rest else []
-        ins.append((op, ops, t))
+        ins.append((op, ops, t, in_asm))
     return ins
 
 
 def check(body):
     ins = parse(body.splitlines())
     bad = []
-    for k, (op, ops, t) in enumerate(ins):
-        if not op.startswith("v_mfma"):
+    for k, (op, ops, t, asm) in enumerate(ins):
+        # hipcc pads its own MFMAs (builtins) through its hazard recognizer; only the MFMAs inside
+        # inline-asm strings are hand-padded
+        if not op.startswith("v_mfma") or not asm:
             continue
         src = regs(ops[1]) | regs(ops[2])
         dist = 0
         for j in range(k - 1, -1, -1):
-            pop, pops, pt = ins[j]
+            pop, pops, pt, _ = ins[j]
             if dist >= 2:
                 break
             if (pop.startswith("v_") and not pop.startswith("v_mfma")) and pops and regs(pops[0]) & src:
@@ -58,7 +66,7 @@ def check(body):
         dst = regs(ops[0])
         dist = 0
         for j in range(k + 1, len(ins)):
-            nop_, nops, nt = ins[j]
+            nop_, nops, nt, _ = ins[j]
             if dist >= 12:
                 break
             if nop_.startswith("v_mfma"):
