@@ -360,7 +360,8 @@ def parity_block(model, dev, cur, ref, oracle_out, inter, R):
     keys = {"mv": ("mvfeature", "quant_mv", 128), "z": ("z", "compressed_z", 64),
             "feature": ("feature", "compressed_feature", 96)}
     st = c["scale_table"].cpu().numpy()
-    par = {"frame": "GOP 0 frame 1 vs frame 0", "latents": {}}
+    from fastvideocodec_amd.net import stream_rows
+    par = {"frame": "GOP 0 frame 1 vs frame 0", "framing": bs.framing, "latents": {}}
     total_sym = total_flip = 0
     t_enc = t_dec = 0.0
     nsym = 0
@@ -374,8 +375,12 @@ def parity_block(model, dev, cur, ref, oracle_out, inter, R):
             gidx = oidx = np.repeat(np.arange(C, dtype=np.int32)[:, None], gsym.shape[1], 1)
         tb = tabs[name]
         strings = getattr(bs, name).to_bytes_list()
+        # one row per stream of the bitstream's framing (segments of a channel row are contiguous)
+        shape = stream_rows(bs.framing, 1, C, gsym.shape[1])
+        gsym, gidx, osym, oidx = (a.reshape(shape) for a in (gsym, gidx, osym, oidx))
+        assert len(strings) == shape[0]
         t1_equal = oracle_equal = 0
-        for ch in range(C):
+        for ch in range(shape[0]):
             t0 = time.perf_counter()
             s_gpu_syms = R.CRef.encode(gsym[ch], gidx[ch], tb.cdf, tb.cdf_length, tb.offset)
             t_enc += time.perf_counter() - t0
@@ -389,7 +394,7 @@ def parity_block(model, dev, cur, ref, oracle_out, inter, R):
         total_flip += flips
         total_sym += gsym.size
         par["latents"][name] = {"symbols": int(gsym.size), "symbol_mismatches": flips,
-                                "index_mismatches": int((gidx != oidx).sum()), "streams": C,
+                                "index_mismatches": int((gidx != oidx).sum()), "streams": shape[0],
                                 "streams_bytes_equal_c_oracle_same_symbols": int(t1_equal),
                                 "streams_bytes_equal_c_oracle_on_oracle_symbols": int(oracle_equal)}
     npx = cur.shape[-1] * cur.shape[-2]
@@ -407,7 +412,8 @@ def parity_block(model, dev, cur, ref, oracle_out, inter, R):
                                       for v in par["latents"].values()),
     })
     coder = {"encode_symbols_per_s": round(nsym / t_enc), "decode_symbols_per_s": round(nsym / t_dec),
-             "symbols": nsym, "note": "oracle/rans_ref.c (-O2), all 288 channel streams of the frame, one core"}
+             "symbols": nsym, "note": f"oracle/rans_ref.c (-O2), all streams of the frame ({bs.framing} framing), "
+                                      f"one core"}
     return par, coder
 
 

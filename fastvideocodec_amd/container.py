@@ -9,7 +9,7 @@ files it deletes (models.py:412-429). Layout (little-endian):
   record  = u8 kind ('I' | 'P') | u16 view | u32 gop | u16 frame | u32 payload_len | payload
   I payload = u16 h | u16 w | u8 levels | u16 q | u32 n_block_idx | block_idx (u8)
               | streams(coefficients)
-  P payload = u8 precision (0 x3, 1 f32) | u8 framing (0 channel, 1 item)
+  P payload = u8 precision (0 x3, 1 f32) | u8 framing (0 channel, 1 item, 2 segment)
               | u16 H/16 | u16 W/16 | u16 H/64 | u16 W/64 | streams(mv) | streams(z) | streams(feature)
   streams = u32 n | u32 len[n] (bytes) | bytes        (each stream byte-identical to compressai's
                                                       RansEncoder.encode_with_indexes output)
@@ -173,7 +173,7 @@ class ContainerReader:
         return sorted({(e[1], e[2]) for e in self.index})
 
 
-def encode_video(model, video: torch.Tensor, f, iframe_q=None, framing="channel", views=None):
+def encode_video(model, video: torch.Tensor, f, iframe_q=None, framing="segment", views=None):
     """Encode video [N, T, 3, H, W] (N GOPs, H and W multiples of 64) into container file f.
     GOP n is muxed as (view = views[n] if given else 0, gop = n). Frame 0 of each GOP is coded by
     the I-frame codec (step iframe_q, default from model.I_level: iframe.iframe_step), frames

@@ -68,8 +68,26 @@ constexpr int kHdr = 512;                             // bias (256 B) + schedule
 constexpr int kLds = kHdr + kRingBytes + 2 * kZBytes; // 148,480 B
 constexpr int kChunk = 16;         // items per schedule chunk (consecutive tile rows of one column)
 constexpr float kLoScale = 2048.f;
+// knock-outs (experiment builds only; results wrong): FVC_WINO_KO bit 1 = no k-step-1 MFMAs,
+// 2 = no k-step-0 MFMAs (their split VALU kept), 4 = no item barrier, 8 = no finishing pass,
+// 16 = finishing pass without its output stores, 32 = finishing pass without its Z reads
+#ifndef FVC_WINO_KO
+#define FVC_WINO_KO 0
+#endif
 #ifndef FVC_WINO_KO_WAIT
 #define FVC_WINO_KO_WAIT 0
+#endif
+#ifndef FVC_WINO_PF
+#define FVC_WINO_PF 0
+#endif
+// packed f32 VALU (v_pk_fma_f32 / v_pk_add_f32: two channels per instruction) in the parts of an
+// item that run outside the MFMA blocks: the transform ahead of them, the column combination and
+// the finishing pass (a lone wave issues one VALU per ~4 cycles whether it is packed or not)
+#ifndef FVC_WINO_PK
+#define FVC_WINO_PK 0
+#endif
+#ifndef FVC_WINO_FM
+#define FVC_WINO_FM 0
 #endif
 #ifndef FVC_WINO_ALLNOP
 #define FVC_WINO_ALLNOP 0
@@ -277,9 +295,12 @@ __global__ __launch_bounds__(256, 1) void conv_wino_kernel(const WinoArgs a) {
   const unsigned yrow_bytes = (unsigned)W * a.yp * 4u;  // one output (and residual) row
   // stage input row iy of image b into ring slot s: one descriptor per row (0 bytes for a
   // padding row), the lane offsets of its column group
-  auto stage_row = [&](int b, int iy, int s, const unsigned (&vo)[3]) {
+  // (ximg: the image's base; a row is one 32 x 32-bit product from it: per-row scalar work stays a
+  // handful of instructions, the 64-bit image offset is formed once per chunk)
+  const unsigned rowe = (unsigned)W * a.xp;
+  auto stage_row = [&](const float* ximg, int iy, int s, const unsigned (&vo)[3]) {
     const bool row_ok = (unsigned)iy < (unsigned)H;
-    const __amdgpu_buffer_rsrc_t rx = rsrc(a.x + ((size_t)b * H + (row_ok ? iy : 0)) * W * a.xp, row_ok ? row_bytes : 0u);
+    const __amdgpu_buffer_rsrc_t rx = rsrc(ximg + (size_t)(unsigned)(row_ok ? iy : 0) * rowe, row_ok ? row_bytes : 0u);
 #pragma unroll
     for (int m = 0; m < 3; ++m) {
       if (m >= npiece) break;
@@ -324,31 +345,55 @@ __global__ __launch_bounds__(256, 1) void conv_wino_kernel(const WinoArgs a) {
   // overflow check: 0 * (pre-activation output) summed over every output; a transformed input
   // >= 65520 rounds to an infinite hi part whose products reach the outputs as inf / NaN
   float chk = 0.f;
+  f2v chk2 = {0.f, 0.f};  // FVC_WINO_PK: the same check, two channels per instruction
   float mxy = 0.f;  // kPostTap: max |y| (y is split into fp16 halves for the tap GEMM)
   // the lane's output byte offsets within an item's 2-row band of column group g, and within a
   // pooled row (past the band for columns outside the image)
+#if FVC_WINO_FM
+  // finishing-pass mapping: wave w -> channel half w & 1 (32 channels) of tile half w >> 1 (8
+  // tiles); lane -> channel quad fq = lane & 7 of that half, tile ft = 8 (w >> 1) + (lane >> 3).
+  // One store instruction then writes, per output pixel, 8 lanes x 16 B = a whole 128-B line
+  // (channel half of a 64-channel pixel) instead of 64-B halves of lines that another wave
+  // completes; the lane reads its (tile, channel quad) entry of the N-tile fn plane (MFMA layout:
+  // entry tile + 16 x quad-within-N-tile)
+  const int fq = lane & 7, ft = 8 * (wave >> 1) + (lane >> 3);
+  const int fn = 2 * (wave & 1) + (fq >> 2);
+  const int fentry = (ft + 16 * (fq & 3)) * 16;
+  const int cbase = 32 * (wave & 1) + 4 * fq;  // = 16 fn + 4 (fq & 3)
+  const int tfin = ft;
+#else
+  const int fn = wave;
+  const int fentry = lane * 16;
   const int cbase = 16 * wave + 4 * o;
+  const int tfin = t;
+#endif
   const int Hp = H >> 1, Wp = W >> 1;
   unsigned yo[2][2], po = 0;
   auto out_offsets = [&](int g) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      const int ox = 32 * g + 2 * t + j;
+      const int ox = 32 * g + 2 * tfin + j;
 #pragma unroll
       for (int i = 0; i < 2; ++i) yo[i][j] = ox < W ? (unsigned)((i * W + ox) * a.yp + cbase) * 4u : kOob;
     }
     if constexpr (POST == kPostPool) {
-      const int px = 16 * g + t;
+      const int px = 16 * g + tfin;
       po = px < Wp ? (unsigned)(px * kC + cbase) * 4u : kOob;
     }
   };
   unsigned vo_cur[3];
+  // image bases of the current chunk (x, the output y / tap partials P, the residual)
+  const unsigned ype = POST == kPostTap ? (unsigned)a.pcp : (unsigned)a.yp;
+  const size_t ximg_e = (size_t)H * W * a.xp, yimg_e = (size_t)H * W * ype;
+  const float* xi_cur = a.x + (size_t)cur.b * ximg_e;
+  float* yi_cur = a.y + (size_t)cur.b * yimg_e;
+  const float* ri_cur = RES ? a.res + (size_t)cur.b * H * W * a.yp : nullptr;
 
   if (cur.ty0 < cur.ty1) {
     // first item of the block: its whole 4-row window into ring slots 0..3
     row_offsets(cur.g, vo_cur);
     out_offsets(cur.g);
-    for (int i = 0; i < 4; ++i) stage_row(cur.b, 2 * cur.ty0 - 1 + i, i, vo_cur);
+    for (int i = 0; i < 4; ++i) stage_row(xi_cur, 2 * cur.ty0 - 1 + i, i, vo_cur);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     int ty = cur.ty0;
@@ -368,11 +413,12 @@ __global__ __launch_bounds__(256, 1) void conv_wino_kernel(const WinoArgs a) {
         if (k == 0 && cont) return;
         const int i0 = 2 * k;
         if (cont) {
-          for (int i = i0; i < i0 + 2; ++i) stage_row(np.b, 2 * nty - 1 + i, (nbase + i) & (kRing - 1), vo_cur);
+          for (int i = i0; i < i0 + 2; ++i) stage_row(xi_cur, 2 * nty - 1 + i, (nbase + i) & (kRing - 1), vo_cur);
         } else {
           unsigned vo[3];
           row_offsets(np.g, vo);
-          for (int i = i0; i < i0 + 2; ++i) stage_row(np.b, 2 * nty - 1 + i, (nbase + i) & (kRing - 1), vo);
+          const float* xi_np = a.x + (size_t)np.b * ximg_e;
+          for (int i = i0; i < i0 + 2; ++i) stage_row(xi_np, 2 * nty - 1 + i, (nbase + i) & (kRing - 1), vo);
         }
       };
       if (first && tid == 0) sq[2 + (ntaken & 1)] = take(ntaken);  // chunk after next
@@ -380,15 +426,13 @@ __global__ __launch_bounds__(256, 1) void conv_wino_kernel(const WinoArgs a) {
       // this lane's 4 output pixels in the finishing pass (channels 16 wave + 4 o .. +3): one
       // descriptor per item over its 2-row band (1 row at an odd image's last tile row); the
       // residual is loaded now so its latency hides behind the k-loop
-      const size_t band = ((size_t)cur.b * H + 2 * ty) * W * a.yp;
       const unsigned band_rows = 2 * ty + 1 < H ? 2u : 1u;
       const unsigned band_bytes = band_rows * yrow_bytes;
-      const __amdgpu_buffer_rsrc_t ry =
-          POST == kPostTap ? rsrc(a.y + ((size_t)cur.b * H + 2 * ty) * W * a.pcp, band_rows * (unsigned)W * a.pcp * 4u)
-                           : rsrc(a.y + band, band_bytes);
+      const __amdgpu_buffer_rsrc_t ry = rsrc(yi_cur + (size_t)(unsigned)(2 * ty) * ((unsigned)W * ype),
+                                             band_rows * (unsigned)W * ype * 4u);
       f32x4 rv[2][2];
       if constexpr (RES) {
-        const __amdgpu_buffer_rsrc_t rr = rsrc(a.res + band, band_bytes);
+        const __amdgpu_buffer_rsrc_t rr = rsrc(ri_cur + (size_t)(unsigned)(2 * ty) * ((unsigned)W * a.yp), band_bytes);
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -433,6 +477,35 @@ __global__ __launch_bounds__(256, 1) void conv_wino_kernel(const WinoArgs a) {
           v[3][4 * hh + c] = e[1] - e[3];
         }
       };
+#if FVC_WINO_PK
+      // the same arithmetic, two channels per instruction (bit-identical: every element is the
+      // same IEEE fma / add)
+      auto transform_pk = [&](const float4 (&da)[4], const float4 (&db)[4], int hh, float (&v)[4][8]) {
+        const f2v sb2 = {sb, sb};
+#pragma unroll
+        for (int cp = 0; cp < 2; ++cp) {
+          f2v e[4];
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj) {
+            f2v xa = cp ? f2v{da[jj].z, da[jj].w} : f2v{da[jj].x, da[jj].y};
+            f2v xb = cp ? f2v{db[jj].z, db[jj].w} : f2v{db[jj].x, db[jj].y};
+            if constexpr (IOP == FVC_IN_RELU) {
+              xa = f2v{relu1(xa.x), relu1(xa.y)};
+              xb = f2v{relu1(xb.x), relu1(xb.y)};
+            }
+            e[jj] = __builtin_elementwise_fma(sb2, xb, xa);
+          }
+          const f2v q0 = e[0] - e[2], q1 = e[1] + e[2], q2 = e[2] - e[1], q3 = e[1] - e[3];
+          v[0][4 * hh + 2 * cp] = q0.x; v[0][4 * hh + 2 * cp + 1] = q0.y;
+          v[1][4 * hh + 2 * cp] = q1.x; v[1][4 * hh + 2 * cp + 1] = q1.y;
+          v[2][4 * hh + 2 * cp] = q2.x; v[2][4 * hh + 2 * cp + 1] = q2.y;
+          v[3][4 * hh + 2 * cp] = q3.x; v[3][4 * hh + 2 * cp + 1] = q3.y;
+        }
+      };
+#define WINO_TRANSFORM transform_pk
+#else
+#define WINO_TRANSFORM transform
+#endif
       auto split_all = [&](const float (&v)[4][8], h8 (&vh)[4], h8 (&vl)[4]) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -452,28 +525,50 @@ __global__ __launch_bounds__(256, 1) void conv_wino_kernel(const WinoArgs a) {
           else wino_mfma3<false, false>(acc[q][n], cor[q][n], u[q][n][1][0], u[q][n][1][1], vh[q], vl[q]);
         }
       };
-      float4 da[4], db[4];
       float v0[4][8], v1[4][8];
       h8 vh0[4], vl0[4], vh1[4], vl1[4];
+#if FVC_WINO_PF
+      // LDS reads one channel half ahead of their transform (two raw buffers): each batch of
+      // ds_reads is in flight while the previous half is transformed instead of waited for
+      float4 da[4], db[4], ea[4], eb[4];
       read_raw(0, 0, da, db);
-      transform(da, db, 0, v0);
+      read_raw(0, 1, ea, eb);
+      WINO_TRANSFORM(da, db, 0, v0);
+      read_raw(1, 0, da, db);
+      WINO_TRANSFORM(ea, eb, 1, v0);
+      read_raw(1, 1, ea, eb);
+      split_all(v0, vh0, vl0);
+      WINO_TRANSFORM(da, db, 0, v1);
+      stage_next(0);
+      WINO_TRANSFORM(ea, eb, 1, v1);
+#else
+      float4 da[4], db[4];
+      read_raw(0, 0, da, db);
+      WINO_TRANSFORM(da, db, 0, v0);
       read_raw(0, 1, da, db);
-      transform(da, db, 1, v0);
+      WINO_TRANSFORM(da, db, 1, v0);
       split_all(v0, vh0, vl0);
       // the next k-step's transform first (its LDS reads were issued ahead), then kk = 0's 16
       // MFMA blocks, each carrying the split of one pair of the next k-step's 32 values
       read_raw(1, 0, da, db);
-      transform(da, db, 0, v1);
+      WINO_TRANSFORM(da, db, 0, v1);
       read_raw(1, 1, da, db);
       stage_next(0);
-      transform(da, db, 1, v1);
+      WINO_TRANSFORM(da, db, 1, v1);
+#endif
       unsigned hw1[4][4], lw1[4][4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
 #pragma unroll
         for (int n = 0; n < 4; ++n)
+          if constexpr (FVC_WINO_KO & 2) {
+            split2(v1[n][2 * q], v1[n][2 * q + 1], hw1[n][q], lw1[n][q]);
+            acc[q][n] = cor[q][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+            asm volatile("" : "+v"(acc[q][n]) : "v"(vh0[q]), "v"(vl0[q]));
+          } else {
           ((q == 0 && n == 0) || kAllNop ? wino_mfma3_split<true> : wino_mfma3_split<false>)(acc[q][n], cor[q][n], u[q][n][0][0], u[q][n][0][1], vh0[q], vl0[q], v1[n][2 * q],
                            v1[n][2 * q + 1], hw1[n][q], lw1[n][q]);
+          }
         if (q == 1) stage_next(1);
       }
 #pragma unroll
@@ -482,7 +577,13 @@ __global__ __launch_bounds__(256, 1) void conv_wino_kernel(const WinoArgs a) {
         vl1[q] = __builtin_bit_cast(h8, v4u{lw1[q][0], lw1[q][1], lw1[q][2], lw1[q][3]});
       }
 #pragma unroll
-      for (int q = 0; q < 4; ++q) mfma_q1(q, vh1, vl1);
+      for (int q = 0; q < 4; ++q) {
+        if constexpr (FVC_WINO_KO & 1) {
+          asm volatile("" : "+v"(acc[q][0]), "+v"(cor[q][0]) : "v"(vh1[q]), "v"(vl1[q]));
+        } else {
+          mfma_q1(q, vh1, vl1);
+        }
+      }
       wino_mfma_drain(acc, cor);
 
       // ---- column combination Z[r][j] = sum_q M[r][q] A[q][j] (M in units of 2^kw: the scale is
@@ -491,6 +592,22 @@ __global__ __launch_bounds__(256, 1) void conv_wino_kernel(const WinoArgs a) {
 #pragma unroll
       for (int n = 0; n < 4; ++n) {
         f32x4 z0, z1;
+#if FVC_WINO_PK
+        const f2v ls2 = {1.f / kLoScale, 1.f / kLoScale};
+#pragma unroll
+        for (int cp = 0; cp < 2; ++cp) {
+          f2v m[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const f2v c2 = cp ? f2v{cor[q][n][2], cor[q][n][3]} : f2v{cor[q][n][0], cor[q][n][1]};
+            const f2v a2 = cp ? f2v{acc[q][n][2], acc[q][n][3]} : f2v{acc[q][n][0], acc[q][n][1]};
+            m[q] = __builtin_elementwise_fma(c2, ls2, a2);
+          }
+          const f2v p0 = (m[0] + m[1]) + m[2], p1 = (m[1] - m[2]) - m[3];
+          z0[2 * cp] = p0.x; z0[2 * cp + 1] = p0.y;
+          z1[2 * cp] = p1.x; z1[2 * cp + 1] = p1.y;
+        }
+#else
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
           float m[4];
@@ -499,6 +616,7 @@ __global__ __launch_bounds__(256, 1) void conv_wino_kernel(const WinoArgs a) {
           z0[c] = (m[0] + m[1]) + m[2];
           z1[c] = (m[1] - m[2]) - m[3];
         }
+#endif
         *reinterpret_cast<f32x4*>(zw + ((wave * 2 + 0) * 4 + n) * 1024 + lane * 16) = z0;
         *reinterpret_cast<f32x4*>(zw + ((wave * 2 + 1) * 4 + n) * 1024 + lane * 16) = z1;
       }
@@ -507,16 +625,22 @@ __global__ __launch_bounds__(256, 1) void conv_wino_kernel(const WinoArgs a) {
 #else
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA pieces of the next item
 #endif
-      __syncthreads();
+      if constexpr (!(FVC_WINO_KO & 4)) __syncthreads();
       if (first) nnp = decode(sq[2 + (ntaken & 1)]);  // published by this item's barrier
 
       // ---- finishing pass: wave w -> output channels 16w..16w+15 of the item's 16 tiles
+      if constexpr (!(FVC_WINO_KO & 8)) {
       f32x4 z[4][2];
 #pragma unroll
       for (int p = 0; p < 4; ++p)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
-          z[p][j] = *reinterpret_cast<const f32x4*>(zw + ((p * 2 + j) * 4 + wave) * 1024 + lane * 16);
+          if constexpr (FVC_WINO_KO & 32) {
+            z[p][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+            asm volatile("" : "+v"(z[p][j]));
+          } else {
+            z[p][j] = *reinterpret_cast<const f32x4*>(zw + ((p * 2 + j) * 4 + fn) * 1024 + fentry);
+          }
       const f32x4 bj = *reinterpret_cast<const f32x4*>(sbias + cbase);
       f32x4 yv[2][2];
 #pragma unroll
@@ -524,6 +648,24 @@ __global__ __launch_bounds__(256, 1) void conv_wino_kernel(const WinoArgs a) {
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
           f32x4 vv;
+#if FVC_WINO_PK
+#pragma unroll
+          for (int cp = 0; cp < 2; ++cp) {
+            auto pr = [&](const f32x4& x) { return cp ? f2v{x[2], x[3]} : f2v{x[0], x[1]}; };
+            const f2v ys = i == 0 ? (pr(z[0][j]) + pr(z[1][j])) + pr(z[2][j]) : (pr(z[1][j]) - pr(z[2][j])) - pr(z[3][j]);
+            chk2 = __builtin_elementwise_fma(ys, f2v{0.f, 0.f}, chk2);
+            f2v tv = __builtin_elementwise_fma(ys, f2v{a.osc, a.osc}, pr(bj));
+            if constexpr (RES == kResPre) tv += pr(rv[i][j]);
+            if constexpr (ACT == FVC_ACT_RELU) tv = f2v{relu1(tv.x), relu1(tv.y)};
+            if constexpr (ACT == FVC_ACT_LRELU) {
+              const f2v t1 = tv * f2v{0.1f, 0.1f};
+              tv = f2v{fmaxf(tv.x, t1.x), fmaxf(tv.y, t1.y)};
+            }
+            if constexpr (RES == kResPost) tv += pr(rv[i][j]);
+            vv[2 * cp] = tv.x;
+            vv[2 * cp + 1] = tv.y;
+          }
+#else
 #pragma unroll
           for (int c = 0; c < 4; ++c) {
             const float ys = i == 0 ? (z[0][j][c] + z[1][j][c]) + z[2][j][c] : (z[1][j][c] - z[2][j][c]) - z[3][j][c];
@@ -535,9 +677,11 @@ __global__ __launch_bounds__(256, 1) void conv_wino_kernel(const WinoArgs a) {
             if constexpr (RES == kResPost) tv += rv[i][j][c];
             vv[c] = tv;
           }
+#endif
           yv[i][j] = vv;
           if constexpr (POST != kPostTap)
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, vv), ry, yo[i][j], 0, FVC_STORE_AUX);
+            if constexpr (FVC_WINO_KO & 16) asm volatile("" ::"v"(vv));
+            else __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, vv), ry, yo[i][j], 0, FVC_STORE_AUX);
         }
       if constexpr (POST == kPostPool) {
         f32x4 pv;
@@ -558,7 +702,7 @@ __global__ __launch_bounds__(256, 1) void conv_wino_kernel(const WinoArgs a) {
         for (int i = 0; i < 2; ++i)
 #pragma unroll
           for (int j = 0; j < 2; ++j) {
-            *reinterpret_cast<f32x4*>(zw + ((i * 2 + j) * 4 + wave) * 1024 + lane * 16) = yv[i][j];
+            *reinterpret_cast<f32x4*>(zw + ((i * 2 + j) * 4 + fn) * 1024 + fentry) = yv[i][j];
 #pragma unroll
             for (int c = 0; c < 4; ++c) mxy = fmaxf(mxy, fabsf(yv[i][j][c]));
           }
@@ -602,6 +746,8 @@ __global__ __launch_bounds__(256, 1) void conv_wino_kernel(const WinoArgs a) {
         }
       }
 
+      }  // FVC_WINO_KO & 8
+
       // ---- advance
       if (!nvalid) break;
       if (!cont) {
@@ -610,6 +756,9 @@ __global__ __launch_bounds__(256, 1) void conv_wino_kernel(const WinoArgs a) {
         ++ntaken;
         row_offsets(cur.g, vo_cur);
         out_offsets(cur.g);
+        xi_cur = a.x + (size_t)cur.b * ximg_e;
+        yi_cur = a.y + (size_t)cur.b * yimg_e;
+        if constexpr (RES != 0) ri_cur = a.res + (size_t)cur.b * H * W * a.yp;
       }
       ty = nty;
       base = nbase;
@@ -617,7 +766,7 @@ __global__ __launch_bounds__(256, 1) void conv_wino_kernel(const WinoArgs a) {
     }
   }
   {
-    if ((chk != 0.f || !(mxy < 65000.f)) && a.ovf) atomicOr(a.ovf, 1);
+    if ((chk != 0.f || chk2.x != 0.f || chk2.y != 0.f || !(mxy < 65000.f)) && a.ovf) atomicOr(a.ovf, 1);
   }
   if (a.sched && tid == 0) {
     __threadfence();

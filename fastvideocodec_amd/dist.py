@@ -4,7 +4,10 @@ GOPs are independent (each starts from its own I-frame; the only dependency, ``x
 a GOP, ``models.py:372-376``), so ranks never exchange data while coding. After coding, one
 collective round moves the small results: the per-rank elapsed time (MAX), per-rank metrics
 (all_gather of a few floats) and every rank's bitstream bytes to rank 0 only (gather of lengths,
-then gather of zero-padded payloads — a few hundred KB per frame, latency-bound on xGMI).
+then gather of payloads zero-padded to the largest rank's). With the seeded (untrained) weights a
+1080p P-frame codes to ~1.3 MB (~5 bpp), so 16 GOPs per rank are ~229 MB per rank and ~1.8 GB
+onto rank 0 at 8 ranks; a trained DVC at 0.137 bpp would be ~36 KB per frame. All of it after the
+timed region.
 Works with ``nccl`` (RCCL on ROCm; device tensors) and ``gloo`` (CPU tensors, tests).
 """
 from __future__ import annotations

@@ -349,20 +349,47 @@ class Synthesis_prior_net(nn.Module):
 
 
 # ------------------------------------------------------------------ the codec
-FRAMINGS = ("channel", "item")
+FRAMINGS = ("channel", "item", "segment")
+# 'segment' framing: each (frame, latent, channel) row of HW symbols is cut into equal contiguous
+# segments of >= 512 symbols (a power-of-two count dividing HW), one rANS stream each. A stream's
+# decode is one sequential chain of symbols, so the chain length sets a frame's decode latency:
+# at 1080p (HW = 68 x 120 = 8160) the mv / feature rows become 8 streams of 1020 symbols. Each
+# stream is still exactly compressai's encode_with_indexes of its symbols (T1 parity per stream);
+# the cost is one rANS flush (4 bytes) per extra stream.
+SEGMENT_MIN = 512
+
+
+def segments(hw: int) -> int:
+    """Streams per (frame, latent, channel) row of hw symbols in the 'segment' framing."""
+    s = 1
+    while s < 64 and hw % (2 * s) == 0 and hw // (2 * s) >= SEGMENT_MIN:
+        s *= 2
+    return s
+
+
+def stream_rows(framing: str, B: int, C: int, hw: int):
+    """(streams, symbols per stream) of a [B, C, hw] latent in a framing (symbols are contiguous
+    per (frame, channel) row, so every framing is a view of the same memory)."""
+    if framing == "item":
+        return B, C * hw
+    if framing == "segment":
+        s = segments(hw)
+        return B * C * s, hw // s
+    return B * C, hw
 
 
 class PFrameBitstream:
     """In-memory P-frame bitstream: three latents (mv, z, feature) of ``batch`` frames.
 
-    framing 'channel' (the codec's default): one rANS stream per (frame, latent, channel), so the
-    decoder runs C-way parallel per frame; 'item': compressai's framing (EntropyModel.compress,
+    framing 'segment' (the codec's default): one rANS stream per contiguous segment of a (frame,
+    latent, channel) row (stream_rows / segments above); 'channel': one stream per (frame, latent,
+    channel), so the decoder runs C-way parallel per frame; 'item': compressai's framing (EntropyModel.compress,
     entropy_models.py:80-86), one stream per (frame, latent) over the whole (C,H,W) latent in C
     order. Either way each stream equals compressai's encode_with_indexes on its symbols.
     precision: the conv precision the encoder's reconstruction used ('x3', or 'f32' when the
     frame was recomputed after a split-precision overflow); the decoder must use the same."""
 
-    def __init__(self, mv, z, feature, batch, hw16, hw64, framing="channel", precision="x3"):
+    def __init__(self, mv, z, feature, batch, hw16, hw64, framing="segment", precision="x3"):
         self.mv, self.z, self.feature = mv, z, feature
         self.batch, self.hw16, self.hw64 = batch, hw16, hw64
         self.framing, self.precision = framing, precision
@@ -533,9 +560,10 @@ class VideoCompressor(nn.Module):
         return (clipped, mse_loss, warploss, interloss, bpp_feature, bpp_z, bpp_mv, bpp), t
 
     # ---------------------------------------------------------------- real bitstream
-    def compress_tensors(self, t, framing="channel") -> PFrameBitstream:
+    def compress_tensors(self, t, framing="segment") -> PFrameBitstream:
         """Range-code the latents of an encoder pass (NHWC device tensors mvfeature, z, feature,
-        sigma). framing: 'channel' (one stream per frame x channel, the codec's default) or 'item'
+        sigma). framing: 'segment' (the codec's default: one stream per contiguous >= 512-symbol
+        segment of a frame x channel row), 'channel' (one stream per frame x channel) or 'item'
         (compressai's one string per frame per latent)."""
         if framing not in FRAMINGS:
             raise ValueError(f"framing must be one of {FRAMINGS}")
@@ -550,13 +578,13 @@ class VideoCompressor(nn.Module):
         idx_z = K.channel_indexes(B, H64 * W64, OUT_CHANNEL_N, sym_z.device)
         idx_f = K.build_indexes(t["sigma"], c["scale_table"], OUT_CHANNEL_M)
         # symbols are [B, C, HW] in memory either way: the framing only chooses the stream cut
-        rows = (lambda C, hw: (B * C, hw)) if framing == "channel" else (lambda C, hw: (B, C * hw))
+        rows = lambda C, hw: stream_rows(framing, B, C, hw)  # noqa: E731
         enc_mv = c["mv"].encode(sym_mv.view(rows(OUT_CHANNEL_MV, H16 * W16)), idx_mv.view(rows(OUT_CHANNEL_MV, H16 * W16)))
         enc_z = c["z"].encode(sym_z.view(rows(OUT_CHANNEL_N, H64 * W64)), idx_z.view(rows(OUT_CHANNEL_N, H64 * W64)))
         enc_f = c["feature"].encode(sym_f.view(rows(OUT_CHANNEL_M, H16 * W16)), idx_f.view(rows(OUT_CHANNEL_M, H16 * W16)))
         return PFrameBitstream(enc_mv, enc_z, enc_f, B, (H16, W16), (H64, W64), framing, K.conv_precision())
 
-    def compress(self, input_image, referframe, return_sse=False, framing="channel"):
+    def compress(self, input_image, referframe, return_sse=False, framing="segment"):
         """Encode one P-frame: returns (bitstream, clipped_recon[, sse]). The recon is what
         ``decompress`` reproduces bit-for-bit; sse = device doubles {recon, warp, pred} SSE."""
         self._check_frames(input_image, referframe)
@@ -582,7 +610,7 @@ class VideoCompressor(nn.Module):
         B = bs.batch
         (H16, W16), (H64, W64) = bs.hw16, bs.hw64
         dev = bs.mv.packed.device
-        rows = (lambda C, hw: (B * C, hw)) if bs.framing == "channel" else (lambda C, hw: (B, C * hw))
+        rows = lambda C, hw: stream_rows(bs.framing, B, C, hw)  # noqa: E731
         with torch.no_grad(), K.precision(bs.precision):
             idx_z = K.channel_indexes(B, H64 * W64, OUT_CHANNEL_N, dev)
             sym_z = c["z"].decode(bs.z, idx_z.view(rows(OUT_CHANNEL_N, H64 * W64)), check).view(B, OUT_CHANNEL_N, H64 * W64)

@@ -1,7 +1,10 @@
 #!/bin/bash
-# conv_wino_kernel knock-out: without the item-end wait for the next item's LDS-DMA rows (wrong results)
+# Knock-out timing of the Winograd kernel (experiment libraries libfvc_wko<K>.so, FVC_WINO_KO=K:
+# results are wrong by construction; conv_micro timings only).
 export TMPDIR=/tmp
-C=c3_64_full,c3_64_full_relu,c3_64_half,c3_64_full_res
-for L in fastvideocodec_amd/libfvc.so fastvideocodec_amd/libfvc_kowait.so; do
-  echo "== $L"; FVC_LIB_PATH=$L timeout -k 10 150 python scripts/conv_micro.py --cases $C --iters 10 --batch 8 2>&1 | grep -v amdgpu.ids || exit 1
-done
+OUT=gpurun_out/${TAG:-wko}; mkdir -p $OUT
+for rep in 1 2; do for k in ${KOS:-0 1 2 3 4 8}; do
+  FVC_LIB_PATH=$PWD/fastvideocodec_amd/libfvc_wko$k.so timeout -k 10 120 python -u scripts/conv_micro.py --batch 8 \
+    --cases c3_64_full,c3_64_full_relu > $OUT/ko${k}_$rep.txt 2>&1 || { tail -20 $OUT/ko${k}_$rep.txt; exit 1; }
+  echo "== KO $k rep $rep"; grep -v amdgpu.ids $OUT/ko${k}_$rep.txt
+done; done

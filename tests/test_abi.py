@@ -223,3 +223,14 @@ def test_x3_layout_id_tracks_layout_switches(monkeypatch):
     assert lib.fvc_conv_x3_layout_id(64, 64, 3, 1, 0) not in (0, wide)
     monkeypatch.setenv("FVC_X3_CIN4", "0")
     assert lib.fvc_conv_x3_layout_id(3, 64, 5, 2, 0) == 0  # back on the fp32 kernels
+
+
+def test_segment_framing_rows():
+    """'segment' framing (the codec's default stream cut): >= 512 symbols per stream, a power-of-two
+    count of equal contiguous segments per (frame, channel) row; the other framings unchanged."""
+    from fastvideocodec_amd.net import segments, stream_rows
+    assert segments(8160) == 8 and segments(32640) == 32 and segments(510) == 1 and segments(256) == 1
+    assert segments(1024) == 2 and segments(1 << 20) == 64
+    assert stream_rows("segment", 2, 128, 8160) == (2 * 128 * 8, 1020)
+    assert stream_rows("channel", 2, 128, 8160) == (256, 8160)
+    assert stream_rows("item", 2, 128, 8160) == (2, 128 * 8160)

@@ -45,20 +45,30 @@ def _tables(model):
     return {"z": tz, "mv": tmv, "feature": tf}
 
 
-def test_compress_1080p_every_stream_vs_oracle(model, dev):
+@pytest.mark.parametrize("framing", ["segment", "channel"])
+def test_compress_1080p_every_stream_vs_oracle(model, dev, framing):
     """BASELINE configs[2]: one 1920x1080 P-frame compressed by the product path; each of its
-    288 channel streams (128 mv + 64 z + 96 feature) equals the C oracle coder's bytes on the
-    same symbols / indexes / tables, the 64 z streams also equal the pure-Python coder's, and the
-    device decoder returns the encoder's symbols."""
+    streams equals the C oracle coder's bytes on the same symbols / indexes / tables, the z
+    streams also equal the pure-Python coder's, and the device decoder returns the encoder's
+    symbols. 'channel': 288 streams (128 mv + 64 z + 96 feature rows of 8160 / 510 symbols);
+    'segment' (the codec's default): every 8160-symbol mv / feature row cut into 8 streams of
+    1020 symbols (1024 + 64 + 768 streams), z rows (510 symbols) left whole."""
+    from fastvideocodec_amd.net import stream_rows
     cur, ref = _frame(dev, 1080, 1920)
     with torch.no_grad():
         t = model._encode_graph(cur, ref)
-    bs = model.compress_tensors(t)
+    bs = model.compress_tensors(t, framing=framing)
+    assert bs.framing == framing
     lat = _latent_symbols(model, t)
     tabs = _tables(model)
     nbytes = 0
+    expect = {"segment": {"mv": 1024, "z": 64, "feature": 768}, "channel": {"mv": 128, "z": 64, "feature": 96}}
     for name in ("mv", "z", "feature"):
         sym, idx = lat[name]
+        C, hw = sym.shape
+        shape = stream_rows(framing, 1, C, hw)
+        assert shape[0] == expect[framing][name], shape
+        sym, idx = sym.reshape(shape), idx.reshape(shape)
         tb = tabs[name]
         strings = getattr(bs, name).to_bytes_list()
         assert len(strings) == sym.shape[0]
