@@ -231,12 +231,14 @@ class RangeCoder:
                   pack_off.data_ptr(), packed.data_ptr(), status.data_ptr(), st)
         return EncodedStreams(packed, pack_off, S, status)
 
-    def decode(self, enc: EncodedStreams, indexes: torch.Tensor, check=True) -> torch.Tensor:
+    def decode(self, enc: EncodedStreams, indexes: torch.Tensor, check=True, defer=None) -> torch.Tensor:
+        """defer: a list to append the device status tensors to instead of checking them here
+        (the caller checks them all with one host wait, e.g. VideoCompressor.decode_latents)."""
         S, n = indexes.shape
         K._chk(indexes, name="indexes", dtype=torch.int32)
         if enc.nstreams != S:
             raise ValueError("stream count mismatch")
-        if check:
+        if check and defer is None:
             enc.check()
         sym_off = self._sym_off(S, n)
         out = torch.empty((S, n), dtype=torch.int32, device=self.device)
@@ -246,7 +248,11 @@ class RangeCoder:
                   self.offset.data_ptr(),
                   self.lut.data_ptr(), out.data_ptr(), status.data_ptr(), K.rans_streams_per_block(),
                   K.stream_handle())
-        if check and int(status.abs().max()) != 0:
+        if check and defer is not None:
+            if enc.status is not None:
+                defer.append(enc.status.view(-1))
+            defer.append(status)
+        elif check and int(status.abs().max()) != 0:
             raise _lib.FvcError("corrupt rANS stream")
         return out
 

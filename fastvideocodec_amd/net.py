@@ -611,17 +611,22 @@ class VideoCompressor(nn.Module):
         (H16, W16), (H64, W64) = bs.hw16, bs.hw64
         dev = bs.mv.packed.device
         rows = lambda C, hw: stream_rows(bs.framing, B, C, hw)  # noqa: E731
+        # stream checks are collected on the device and read once at the end (one host wait per
+        # frame instead of two per latent)
+        st = [] if check else None
         with torch.no_grad(), K.precision(bs.precision):
             idx_z = K.channel_indexes(B, H64 * W64, OUT_CHANNEL_N, dev)
-            sym_z = c["z"].decode(bs.z, idx_z.view(rows(OUT_CHANNEL_N, H64 * W64)), check).view(B, OUT_CHANNEL_N, H64 * W64)
+            sym_z = c["z"].decode(bs.z, idx_z.view(rows(OUT_CHANNEL_N, H64 * W64)), check, st).view(B, OUT_CHANNEL_N, H64 * W64)
             z = K.symbols_to_latent(sym_z, H64, W64, OUT_CHANNEL_N)
             sigma = self.respriorDecoder.run(z)
             idx_f = K.build_indexes(sigma, c["scale_table"], OUT_CHANNEL_M)
-            sym_f = c["feature"].decode(bs.feature, idx_f.view(rows(OUT_CHANNEL_M, H16 * W16)), check).view(B, OUT_CHANNEL_M, H16 * W16)
+            sym_f = c["feature"].decode(bs.feature, idx_f.view(rows(OUT_CHANNEL_M, H16 * W16)), check, st).view(B, OUT_CHANNEL_M, H16 * W16)
             feature = K.symbols_to_latent(sym_f, H16, W16, OUT_CHANNEL_M)
             idx_mv = K.channel_indexes(B, H16 * W16, OUT_CHANNEL_MV, dev)
-            sym_mv = c["mv"].decode(bs.mv, idx_mv.view(rows(OUT_CHANNEL_MV, H16 * W16)), check).view(B, OUT_CHANNEL_MV, H16 * W16)
+            sym_mv = c["mv"].decode(bs.mv, idx_mv.view(rows(OUT_CHANNEL_MV, H16 * W16)), check, st).view(B, OUT_CHANNEL_MV, H16 * W16)
             mvq = K.symbols_to_latent(sym_mv, H16, W16, OUT_CHANNEL_MV)
+        if st and int(torch.cat(st).abs().max()) != 0:
+            raise FvcError("corrupt rANS stream (or a failed encode)")
         return {"mv": mvq, "feature": feature, "z": z, "precision": bs.precision}
 
     def reconstruct(self, lat, referframe):
