@@ -77,18 +77,6 @@ constexpr float kLoScale = 2048.f;
 #ifndef FVC_WINO_KO_WAIT
 #define FVC_WINO_KO_WAIT 0
 #endif
-#ifndef FVC_WINO_PF
-#define FVC_WINO_PF 0
-#endif
-// packed f32 VALU (v_pk_fma_f32 / v_pk_add_f32: two channels per instruction) in the parts of an
-// item that run outside the MFMA blocks: the transform ahead of them, the column combination and
-// the finishing pass (a lone wave issues one VALU per ~4 cycles whether it is packed or not)
-#ifndef FVC_WINO_PK
-#define FVC_WINO_PK 0
-#endif
-#ifndef FVC_WINO_FM
-#define FVC_WINO_FM 0
-#endif
 #ifndef FVC_WINO_ALLNOP
 #define FVC_WINO_ALLNOP 0
 #endif
@@ -344,40 +332,22 @@ __global__ __launch_bounds__(256, 1) void conv_wino_kernel(const WinoArgs a) {
 
   // overflow check: 0 * (pre-activation output) summed over every output; a transformed input
   // >= 65520 rounds to an infinite hi part whose products reach the outputs as inf / NaN
-  float chk = 0.f;
-  f2v chk2 = {0.f, 0.f};  // FVC_WINO_PK: the same check, two channels per instruction
+  f2v chk2 = {0.f, 0.f};  // overflow check, two channels per instruction
   float mxy = 0.f;  // kPostTap: max |y| (y is split into fp16 halves for the tap GEMM)
   // the lane's output byte offsets within an item's 2-row band of column group g, and within a
   // pooled row (past the band for columns outside the image)
-#if FVC_WINO_FM
-  // finishing-pass mapping: wave w -> channel half w & 1 (32 channels) of tile half w >> 1 (8
-  // tiles); lane -> channel quad fq = lane & 7 of that half, tile ft = 8 (w >> 1) + (lane >> 3).
-  // One store instruction then writes, per output pixel, 8 lanes x 16 B = a whole 128-B line
-  // (channel half of a 64-channel pixel) instead of 64-B halves of lines that another wave
-  // completes; the lane reads its (tile, channel quad) entry of the N-tile fn plane (MFMA layout:
-  // entry tile + 16 x quad-within-N-tile)
-  const int fq = lane & 7, ft = 8 * (wave >> 1) + (lane >> 3);
-  const int fn = 2 * (wave & 1) + (fq >> 2);
-  const int fentry = (ft + 16 * (fq & 3)) * 16;
-  const int cbase = 32 * (wave & 1) + 4 * fq;  // = 16 fn + 4 (fq & 3)
-  const int tfin = ft;
-#else
-  const int fn = wave;
-  const int fentry = lane * 16;
   const int cbase = 16 * wave + 4 * o;
-  const int tfin = t;
-#endif
   const int Hp = H >> 1, Wp = W >> 1;
   unsigned yo[2][2], po = 0;
   auto out_offsets = [&](int g) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      const int ox = 32 * g + 2 * tfin + j;
+      const int ox = 32 * g + 2 * t + j;
 #pragma unroll
       for (int i = 0; i < 2; ++i) yo[i][j] = ox < W ? (unsigned)((i * W + ox) * a.yp + cbase) * 4u : kOob;
     }
     if constexpr (POST == kPostPool) {
-      const int px = 16 * g + tfin;
+      const int px = 16 * g + t;
       po = px < Wp ? (unsigned)(px * kC + cbase) * 4u : kOob;
     }
   };
@@ -458,28 +428,10 @@ __global__ __launch_bounds__(256, 1) void conv_wino_kernel(const WinoArgs a) {
         db[2] = *reinterpret_cast<const float4*>(rowb + e0 + 16);
         db[3] = *reinterpret_cast<const float4*>(rowb + e0 + 18 * 16);
       };
-      auto transform = [&](const float4 (&da)[4], const float4 (&db)[4], int hh, float (&v)[4][8]) {
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          float e[4];
-#pragma unroll
-          for (int jj = 0; jj < 4; ++jj) {
-            float xa = da[jj][c], xb = db[jj][c];
-            if constexpr (IOP == FVC_IN_RELU) {
-              xa = relu1(xa);
-              xb = relu1(xb);
-            }
-            e[jj] = fmaf(sb, xb, xa);
-          }
-          v[0][4 * hh + c] = e[0] - e[2];
-          v[1][4 * hh + c] = e[1] + e[2];
-          v[2][4 * hh + c] = e[2] - e[1];
-          v[3][4 * hh + c] = e[1] - e[3];
-        }
-      };
-#if FVC_WINO_PK
-      // the same arithmetic, two channels per instruction (bit-identical: every element is the
-      // same IEEE fma / add)
+      // V[q] = E B of the lane's tile for 4 channels (E = d[ra] + sb d[rb]), two channels per packed
+      // instruction (v_pk_fma_f32 / v_pk_add_f32; a lone wave issues one VALU per ~4 cycles whether
+      // packed or not: packing the transform, the column combination and the finishing pass, the
+      // parts outside the MFMA blocks, gained 2-3 %, profiles/r4/wino_pk)
       auto transform_pk = [&](const float4 (&da)[4], const float4 (&db)[4], int hh, float (&v)[4][8]) {
         const f2v sb2 = {sb, sb};
 #pragma unroll
@@ -502,10 +454,6 @@ __global__ __launch_bounds__(256, 1) void conv_wino_kernel(const WinoArgs a) {
           v[3][4 * hh + 2 * cp] = q3.x; v[3][4 * hh + 2 * cp + 1] = q3.y;
         }
       };
-#define WINO_TRANSFORM transform_pk
-#else
-#define WINO_TRANSFORM transform
-#endif
       auto split_all = [&](const float (&v)[4][8], h8 (&vh)[4], h8 (&vl)[4]) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -527,35 +475,19 @@ __global__ __launch_bounds__(256, 1) void conv_wino_kernel(const WinoArgs a) {
       };
       float v0[4][8], v1[4][8];
       h8 vh0[4], vl0[4], vh1[4], vl1[4];
-#if FVC_WINO_PF
       // LDS reads one channel half ahead of their transform (two raw buffers): each batch of
       // ds_reads is in flight while the previous half is transformed instead of waited for
       float4 da[4], db[4], ea[4], eb[4];
       read_raw(0, 0, da, db);
       read_raw(0, 1, ea, eb);
-      WINO_TRANSFORM(da, db, 0, v0);
+      transform_pk(da, db, 0, v0);
       read_raw(1, 0, da, db);
-      WINO_TRANSFORM(ea, eb, 1, v0);
+      transform_pk(ea, eb, 1, v0);
       read_raw(1, 1, ea, eb);
       split_all(v0, vh0, vl0);
-      WINO_TRANSFORM(da, db, 0, v1);
+      transform_pk(da, db, 0, v1);
       stage_next(0);
-      WINO_TRANSFORM(ea, eb, 1, v1);
-#else
-      float4 da[4], db[4];
-      read_raw(0, 0, da, db);
-      WINO_TRANSFORM(da, db, 0, v0);
-      read_raw(0, 1, da, db);
-      WINO_TRANSFORM(da, db, 1, v0);
-      split_all(v0, vh0, vl0);
-      // the next k-step's transform first (its LDS reads were issued ahead), then kk = 0's 16
-      // MFMA blocks, each carrying the split of one pair of the next k-step's 32 values
-      read_raw(1, 0, da, db);
-      WINO_TRANSFORM(da, db, 0, v1);
-      read_raw(1, 1, da, db);
-      stage_next(0);
-      WINO_TRANSFORM(da, db, 1, v1);
-#endif
+      transform_pk(ea, eb, 1, v1);
       unsigned hw1[4][4], lw1[4][4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
@@ -592,7 +524,6 @@ __global__ __launch_bounds__(256, 1) void conv_wino_kernel(const WinoArgs a) {
 #pragma unroll
       for (int n = 0; n < 4; ++n) {
         f32x4 z0, z1;
-#if FVC_WINO_PK
         const f2v ls2 = {1.f / kLoScale, 1.f / kLoScale};
 #pragma unroll
         for (int cp = 0; cp < 2; ++cp) {
@@ -607,16 +538,6 @@ __global__ __launch_bounds__(256, 1) void conv_wino_kernel(const WinoArgs a) {
           z0[2 * cp] = p0.x; z0[2 * cp + 1] = p0.y;
           z1[2 * cp] = p1.x; z1[2 * cp + 1] = p1.y;
         }
-#else
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          float m[4];
-#pragma unroll
-          for (int q = 0; q < 4; ++q) m[q] = fmaf(cor[q][n][c], 1.f / kLoScale, acc[q][n][c]);
-          z0[c] = (m[0] + m[1]) + m[2];
-          z1[c] = (m[1] - m[2]) - m[3];
-        }
-#endif
         *reinterpret_cast<f32x4*>(zw + ((wave * 2 + 0) * 4 + n) * 1024 + lane * 16) = z0;
         *reinterpret_cast<f32x4*>(zw + ((wave * 2 + 1) * 4 + n) * 1024 + lane * 16) = z1;
       }
@@ -639,7 +560,7 @@ __global__ __launch_bounds__(256, 1) void conv_wino_kernel(const WinoArgs a) {
             z[p][j] = f32x4{0.f, 0.f, 0.f, 0.f};
             asm volatile("" : "+v"(z[p][j]));
           } else {
-            z[p][j] = *reinterpret_cast<const f32x4*>(zw + ((p * 2 + j) * 4 + fn) * 1024 + fentry);
+            z[p][j] = *reinterpret_cast<const f32x4*>(zw + ((p * 2 + j) * 4 + wave) * 1024 + lane * 16);
           }
       const f32x4 bj = *reinterpret_cast<const f32x4*>(sbias + cbase);
       f32x4 yv[2][2];
@@ -648,7 +569,6 @@ __global__ __launch_bounds__(256, 1) void conv_wino_kernel(const WinoArgs a) {
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
           f32x4 vv;
-#if FVC_WINO_PK
 #pragma unroll
           for (int cp = 0; cp < 2; ++cp) {
             auto pr = [&](const f32x4& x) { return cp ? f2v{x[2], x[3]} : f2v{x[0], x[1]}; };
@@ -665,23 +585,11 @@ __global__ __launch_bounds__(256, 1) void conv_wino_kernel(const WinoArgs a) {
             vv[2 * cp] = tv.x;
             vv[2 * cp + 1] = tv.y;
           }
-#else
-#pragma unroll
-          for (int c = 0; c < 4; ++c) {
-            const float ys = i == 0 ? (z[0][j][c] + z[1][j][c]) + z[2][j][c] : (z[1][j][c] - z[2][j][c]) - z[3][j][c];
-            chk = fmaf(ys, 0.f, chk);
-            float tv = fmaf(ys, a.osc, bj[c]);
-            if constexpr (RES == kResPre) tv += rv[i][j][c];
-            if constexpr (ACT == FVC_ACT_RELU) tv = relu1(tv);
-            if constexpr (ACT == FVC_ACT_LRELU) tv = fmaxf(tv, 0.1f * tv);
-            if constexpr (RES == kResPost) tv += rv[i][j][c];
-            vv[c] = tv;
-          }
-#endif
           yv[i][j] = vv;
-          if constexpr (POST != kPostTap)
+          if constexpr (POST != kPostTap) {
             if constexpr (FVC_WINO_KO & 16) asm volatile("" ::"v"(vv));
             else __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, vv), ry, yo[i][j], 0, FVC_STORE_AUX);
+          }
         }
       if constexpr (POST == kPostPool) {
         f32x4 pv;
@@ -702,7 +610,7 @@ __global__ __launch_bounds__(256, 1) void conv_wino_kernel(const WinoArgs a) {
         for (int i = 0; i < 2; ++i)
 #pragma unroll
           for (int j = 0; j < 2; ++j) {
-            *reinterpret_cast<f32x4*>(zw + ((i * 2 + j) * 4 + fn) * 1024 + fentry) = yv[i][j];
+            *reinterpret_cast<f32x4*>(zw + ((i * 2 + j) * 4 + wave) * 1024 + lane * 16) = yv[i][j];
 #pragma unroll
             for (int c = 0; c < 4; ++c) mxy = fmaxf(mxy, fabsf(yv[i][j][c]));
           }
@@ -766,7 +674,7 @@ __global__ __launch_bounds__(256, 1) void conv_wino_kernel(const WinoArgs a) {
     }
   }
   {
-    if ((chk != 0.f || chk2.x != 0.f || chk2.y != 0.f || !(mxy < 65000.f)) && a.ovf) atomicOr(a.ovf, 1);
+    if ((chk2.x != 0.f || chk2.y != 0.f || !(mxy < 65000.f)) && a.ovf) atomicOr(a.ovf, 1);
   }
   if (a.sched && tid == 0) {
     __threadfence();
