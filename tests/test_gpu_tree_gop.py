@@ -57,11 +57,11 @@ def test_tree_gop_vs_oracle(model, dev, seeded_sd):
     * open loop, every frame: the oracle codes frame t against the device's reconstruction of its
       parent; symbols equal (flip rate <= 1e-3, 0 observed at these sizes) and, on identical
       symbols, the clipped recon within 4e-5 abs and PSNR within 1e-4 dB;
-    * closed loop: the oracle runs the whole tree on its own reconstructions; per-frame PSNR
-      stays within 5e-3 dB of the device's (measured r3: 1.1e-3 dB at frame 10, depth 3 of the
-      tree, after the Winograd kernel changed the last bits of the Warp_net convs; open-loop
-      differences compound down a tree path as in the sequential chain, test_gpu_forward's
-      closed-loop bound is 2e-2 dB)."""
+    * closed loop: the oracle runs the whole tree on its own reconstructions; the device's
+      per-frame PSNR drift from it may not exceed twice the drift of the fp32-MFMA convs on the
+      same tree (or 1e-4 dB): open-loop ulp differences compound down a tree path the way the
+      reference's own cross-backend runs drift, so the bound is anchored to a plain
+      fp32 implementation rather than to a constant (r3 measured 1.1e-3 dB at frame 10)."""
     from oracle import dvc_ref
     T = 12
     frames = torch.from_numpy(np.stack([make_gop(128, 192, T, 77)])).to(dev)
