@@ -7,14 +7,14 @@ export TMPDIR=/tmp
 RND=${1:-r2}
 OUT=gpurun_out/prof_$RND
 mkdir -p $OUT
-CMD="python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --serial"
+CMD="python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-ref-metrics --serial"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/stats -o run -- $CMD \
   --json-out $OUT/bench_serial.json > $OUT/stats.log 2>&1 || { tail -20 $OUT/stats.log; exit 1; }
 echo "stats done"
 timeout -s KILL 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- \
-  python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --serial > $OUT/fetch.log 2>&1 || { tail -20 $OUT/fetch.log; exit 1; }
+  python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-ref-metrics --serial > $OUT/fetch.log 2>&1 || { tail -20 $OUT/fetch.log; exit 1; }
 echo "fetch done"
 timeout -s KILL 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- \
-  python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --serial > $OUT/write.log 2>&1 || { tail -20 $OUT/write.log; exit 1; }
+  python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-ref-metrics --serial > $OUT/write.log 2>&1 || { tail -20 $OUT/write.log; exit 1; }
 echo "write done"
 find $OUT -name "*.csv" | head -20
