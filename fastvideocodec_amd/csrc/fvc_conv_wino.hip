@@ -74,11 +74,6 @@ constexpr float kLoScale = 2048.f;
 #ifndef FVC_WINO_KO
 #define FVC_WINO_KO 0
 #endif
-// FVC_WINO_DS (experiment): item k's four output stores deferred into item k + 1's MFMA blocks
-// (1: k-step 0's, 2: k-step 1's) instead of ending item k's finishing pass
-#ifndef FVC_WINO_DS
-#define FVC_WINO_DS 0
-#endif
 #ifndef FVC_WINO_KO_WAIT
 #define FVC_WINO_KO_WAIT 0
 #endif
@@ -374,18 +369,6 @@ __global__ __launch_bounds__(256, 1) void conv_wino_kernel(const WinoArgs a) {
     int ty = cur.ty0;
     int base = 0;  // ring slot of the current item's first row
     int zb = 0;    // Z buffer
-    // FVC_WINO_DS: the previous item's outputs, stored during this item's MFMA blocks
-    constexpr bool kDS = FVC_WINO_DS != 0 && POST != kPostTap;
-    f32x4 dv[2][2];
-    unsigned dvo[2][2];
-    __amdgpu_buffer_rsrc_t dry;
-    bool dpend = false;
-    auto dstore = [&](int q) {
-      if constexpr (kDS) {
-        if (dpend) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, dv[q >> 1][q & 1]), dry,
-                                                          dvo[q >> 1][q & 1], 0, FVC_STORE_AUX);
-      }
-    };
     for (;;) {
       const bool first = ty == cur.ty0;
       const bool cont = ty + 1 < cur.ty1;  // the next item continues down this column: 2 new rows
@@ -519,7 +502,6 @@ __global__ __launch_bounds__(256, 1) void conv_wino_kernel(const WinoArgs a) {
                            v1[n][2 * q + 1], hw1[n][q], lw1[n][q]);
           }
         if (q == 1) stage_next(1);
-        if constexpr (FVC_WINO_DS == 1) dstore(q);
       }
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
@@ -528,7 +510,6 @@ __global__ __launch_bounds__(256, 1) void conv_wino_kernel(const WinoArgs a) {
       }
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        if constexpr (FVC_WINO_DS == 2) dstore(q);
         if constexpr (FVC_WINO_KO & 1) {
           asm volatile("" : "+v"(acc[q][0]), "+v"(cor[q][0]) : "v"(vh1[q]), "v"(vl1[q]));
         } else {
@@ -605,10 +586,7 @@ __global__ __launch_bounds__(256, 1) void conv_wino_kernel(const WinoArgs a) {
             vv[2 * cp + 1] = tv.y;
           }
           yv[i][j] = vv;
-          if constexpr (kDS) {
-            dv[i][j] = vv;
-            dvo[i][j] = yo[i][j];
-          } else if constexpr (POST != kPostTap) {
+          if constexpr (POST != kPostTap) {
             if constexpr (FVC_WINO_KO & 16) asm volatile("" ::"v"(vv));
             else __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, vv), ry, yo[i][j], 0, FVC_STORE_AUX);
           }
@@ -678,17 +656,8 @@ __global__ __launch_bounds__(256, 1) void conv_wino_kernel(const WinoArgs a) {
 
       }  // FVC_WINO_KO & 8
 
-      if constexpr (kDS) {
-        dry = ry;
-        dpend = true;
-      }
       // ---- advance
-      if (!nvalid) {
-        if constexpr (kDS) {
-          for (int q = 0; q < 4; ++q) dstore(q);
-        }
-        break;
-      }
+      if (!nvalid) break;
       if (!cont) {
         cur = nxt;
         nxt = nnp;
