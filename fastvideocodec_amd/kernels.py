@@ -197,7 +197,7 @@ def rans_streams_per_block() -> int:
 @contextlib.contextmanager
 def rans_throughput(on: bool = True):
     old = _STATE["rans_spb"]
-    _STATE["rans_spb"] = 64 if on else old
+    _STATE["rans_spb"] = int(os.environ.get("FVC_RANS_SPB_PIPE", "64")) if on else old
     try:
         yield
     finally:
