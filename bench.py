@@ -752,11 +752,12 @@ def parse_args(argv=None):
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--gop", type=int, default=12)
-    ap.add_argument("--gops-per-gpu", type=int, default=16,
+    ap.add_argument("--gops-per-gpu", type=int, default=None,
                     help="GOPs batched per rank per step (SURVEY §8(e)); default 16 x 2 steps = 32 GOPs per run "
-                         "(§8(d)). Measured on MI355X (3 steps): r2 4 -> 56.1, 8 -> 58.2-58.9, 16 -> 59.3; r3 "
-                         "8 -> 68.92/68.84, 16 -> 69.92/69.95/69.91, 24 -> 68.13, 32 -> 68.22 P-frames/s "
-                         "(profiles/r3/gops_sweep)")
+                         "(§8(d)), 4 with --tree (a tree layer batches up to 6 frames per GOP: 16 GOPs would "
+                         "need ~50 GB per 1080p activation). Measured on MI355X: r3 8 -> 68.92/68.84, 16 -> "
+                         "69.92/69.95/69.91, 24 -> 68.13, 32 -> 68.22 P-frames/s (profiles/r3/gops_sweep); r4 "
+                         "12 -> 71.27/71.30, 16 -> 73.34/73.23, 24 -> 70.06/69.94 (profiles/r4/gops_sweep)")
     ap.add_argument("--views", type=int, default=0,
                     help="BASELINE configs[4]: V camera views, one GOP stream each, view v -> rank v %% world "
                          "(replaces --gops-per-gpu; the reference's MCVC couples views, DVC views are independent)")
@@ -781,6 +782,8 @@ def parse_args(argv=None):
     args = ap.parse_args(argv)
     if args.no_cpu_baseline:
         args.cpu_baseline = "none"
+    if args.gops_per_gpu is None:
+        args.gops_per_gpu = 4 if args.tree else 16
     return args
 
 

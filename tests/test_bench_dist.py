@@ -166,3 +166,12 @@ def test_bench_tree_labels_extension(tmp_path):
     res = _run_bench_cli(["--tree", "--gop", "12", "--gops-per-gpu", "1", "--steps", "1", "--warmup", "0",
                           "--height", "64", "--width", "128", "--cpu-baseline", "none"], tmp_path)
     assert res["config"]["tree"]["layers"] == [[1, 8], [2, 5, 9], [3, 4, 6, 7, 10, 11]]
+
+
+def test_gops_per_gpu_defaults():
+    """16 GOPs per step for the sequential GOP; 4 for --tree (its layers batch up to 6 frames per
+    GOP); an explicit value wins either way."""
+    import bench
+    assert bench.parse_args([]).gops_per_gpu == 16
+    assert bench.parse_args(["--tree"]).gops_per_gpu == 4
+    assert bench.parse_args(["--tree", "--gops-per-gpu", "8"]).gops_per_gpu == 8
