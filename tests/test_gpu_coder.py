@@ -167,6 +167,44 @@ def test_rans_encoder_empty_stream_flushes_state(dev):
     assert len(s) == 8
 
 
+def test_rans_decode_damaged_streams(dev):
+    """Damaged input to the device decoder (compressai's RansDecoder has no error detection; this
+    decoder bounds every read by the stream's own word count and reports ECORRUPT per stream):
+    * a stream cut short by its last word fails with FvcError (the renorm that needs the word
+      finds the stream exhausted), and so does an empty (0-word) stream;
+    * words flipped inside one stream change only that stream's symbols: every other stream of
+      the launch still decodes to its exact symbols, whatever the damaged one yields;
+    * the launch completes either way (no fault, no hang: the decoder's reads never leave the
+      packed buffer)."""
+    from fastvideocodec_amd._lib import FvcError
+    lap = EM.LaplaceTables()
+    rc = EM.RangeCoder(lap.cdf, lap.cdf_length, lap.offset, dev)
+    g = np.random.default_rng(5)
+    S, n = 96, 1020
+    idx = g.integers(0, lap.cdf.shape[0], (S, n)).astype(np.int32)
+    sym = np.rint(g.laplace(0, 3, (S, n))).astype(np.int32)
+    idx_d, sym_d = torch.from_numpy(idx).to(dev), torch.from_numpy(sym).to(dev)
+    strings = rc.encode(sym_d, idx_d).to_bytes_list()
+    assert torch.equal(rc.decode(EM.EncodedStreams.from_bytes_list(strings, dev), idx_d).cpu(), sym_d.cpu())
+    for cut in (4, len(strings[17])):  # one word short; the whole stream gone
+        bad = list(strings)
+        bad[17] = strings[17][: len(strings[17]) - cut]
+        with pytest.raises(FvcError):
+            rc.decode(EM.EncodedStreams.from_bytes_list(bad, dev), idx_d)
+        torch.cuda.synchronize()
+    for victim in (0, 40, S - 1):
+        bad = list(strings)
+        w = bytearray(strings[victim])
+        for k in range(8, len(w) - 4, 97):
+            w[k] ^= 0xA5
+        bad[victim] = bytes(w)
+        out = rc.decode(EM.EncodedStreams.from_bytes_list(bad, dev), idx_d, check=False).cpu()
+        torch.cuda.synchronize()
+        keep = [i for i in range(S) if i != victim]
+        assert torch.equal(out[keep], sym_d.cpu()[keep]), victim
+        assert not torch.equal(out[victim], sym_d.cpu()[victim]), victim
+
+
 def _overflowing_model(dev, policy):
     """Seeded weights with Warp_net's last ResBlock's first conv scaled by 1e7: its output (the
     next conv's input) leaves the split-precision range (|v| >= 65000)."""
