@@ -297,6 +297,24 @@ __device__ __forceinline__ float4 warp_sample4(const float* im, size_t bbase, in
   return o;
 }
 
+// warp_sample4 with every tap loaded unconditionally (an out-of-image tap reads the clamped edge
+// pixel): when x0 + 1 == W the border clamp made ix == W - 1 exactly, so the east weights are 0 and
+// the tap adds 0 * v where warp_sample4 adds 0 * 0: the same values for finite images (a zero can
+// only differ in sign, and only in an exactly-zero sum); no branches, so the compiler can count the
+// loads in flight exactly
+__device__ __forceinline__ float4 warp_sample4_nb(const float4* __restrict__ s, unsigned bbase, int W, int H,
+                                                  const WarpTap& t) {
+  const unsigned r0 = bbase + (unsigned)t.y0 * W + t.x0;
+  const unsigned dx = t.vx1 ? 1u : 0u, dy = t.vy1 ? (unsigned)W : 0u;
+  const float4 vnw = s[r0], vne = s[r0 + dx], vsw = s[r0 + dy], vse = s[r0 + dy + dx];
+  float4 o;
+  o.x = ((vnw.x * t.nw + vne.x * t.ne) + vsw.x * t.sw) + vse.x * t.se;
+  o.y = ((vnw.y * t.nw + vne.y * t.ne) + vsw.y * t.sw) + vse.y * t.se;
+  o.z = ((vnw.z * t.nw + vne.z * t.ne) + vsw.z * t.sw) + vse.z * t.se;
+  o.w = ((vnw.w * t.nw + vne.w * t.ne) + vsw.w * t.sw) + vse.w * t.se;
+  return o;
+}
+
 __global__ void k_warp(const float* __restrict__ im, const float* __restrict__ flow, float* __restrict__ out,
                        int B, int H, int W, int cp) {
   const int c4n = cp / 4;
@@ -417,48 +435,139 @@ __global__ void k_up2_add(const float* __restrict__ src, const float* __restrict
 }
 
 // ------------------------------------------------------------------ SpyNet level assembly
+__device__ __forceinline__ void spynet_assemble_px(const float* __restrict__ im1, const float* __restrict__ im2,
+                                                   const float* __restrict__ flow_prev, float* __restrict__ flow_up,
+                                                   float* __restrict__ x8, size_t p, int x, int y, size_t b, int H,
+                                                   int W) {
+  const int h = H / 2, w = W / 2;
+  float4 fu = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (flow_prev) {
+    const UpIdx uy = up_index(y, h, H, 0), ux = up_index(x, w, W, 0);
+    fu = up_sample4(flow_prev, b * h * w, w, 1, 0, uy, ux);
+    fu.x = fu.x * 2.f; fu.y = fu.y * 2.f; fu.z = 0.f; fu.w = 0.f;
+  }
+  reinterpret_cast<float4*>(flow_up)[p] = fu;
+  const WarpTap t = warp_tap(y, x, fu.x, fu.y, H, W);
+  const float4 wv = warp_sample4(im2, b * H * W, W, 1, 0, t);
+  const float4 a = reinterpret_cast<const float4*>(im1)[p];
+  float4* o = reinterpret_cast<float4*>(x8) + p * 2;
+  o[0] = make_float4(a.x, a.y, a.z, wv.x);
+  o[1] = make_float4(wv.y, wv.z, fu.x, fu.y);
+}
+
 __global__ void k_spynet_assemble(const float* __restrict__ im1, const float* __restrict__ im2,
                                   const float* __restrict__ flow_prev, float* __restrict__ flow_up,
                                   float* __restrict__ x8, int B, int H, int W) {
   const size_t npix = (size_t)B * H * W;
+  for (size_t p = grid_stride_start(); p < npix; p += (size_t)gridDim.x * blockDim.x)
+    spynet_assemble_px(im1, im2, flow_prev, flow_up, x8, p, p % W, (p / W) % H, p / ((size_t)H * W), H, W);
+}
+
+// 32-bit forms of the pixel-walking kernels (B*H*W*2 < 2^32): the pixel -> (b, y, x) split as two
+// multiply-high divisions by host-computed magic numbers (udiv_magic) instead of three 64-bit
+// divisions per pixel; the per-pixel arithmetic is the 64-bit kernels' (same device functions)
+__global__ void k_spynet_assemble_q(const float* __restrict__ im1, const float* __restrict__ im2,
+                                    const float* __restrict__ flow_prev, float* __restrict__ flow_up,
+                                    float* __restrict__ x8, int B, int H, int W, unsigned mW, unsigned mH) {
+  const unsigned npix = (unsigned)B * H * W;
+  const unsigned st = gridDim.x * blockDim.x;
   const int h = H / 2, w = W / 2;
-  for (size_t p = grid_stride_start(); p < npix; p += (size_t)gridDim.x * blockDim.x) {
-    const int x = p % W;
-    const int y = (p / W) % H;
-    const size_t b = p / ((size_t)H * W);
-    float4 fu = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (flow_prev) {
-      const UpIdx uy = up_index(y, h, H, 0), ux = up_index(x, w, W, 0);
-      fu = up_sample4(flow_prev, b * h * w, w, 1, 0, uy, ux);
-      fu.x = fu.x * 2.f; fu.y = fu.y * 2.f; fu.z = 0.f; fu.w = 0.f;
-    }
-    reinterpret_cast<float4*>(flow_up)[p] = fu;
-    const WarpTap t = warp_tap(y, x, fu.x, fu.y, H, W);
-    const float4 wv = warp_sample4(im2, b * H * W, W, 1, 0, t);
-    const float4 a = reinterpret_cast<const float4*>(im1)[p];
-    float4* o = reinterpret_cast<float4*>(x8) + p * 2;
-    o[0] = make_float4(a.x, a.y, a.z, wv.x);
-    o[1] = make_float4(wv.y, wv.z, fu.x, fu.y);
+  const float4* const f4 = reinterpret_cast<const float4*>(flow_prev);
+  const float4* const i2 = reinterpret_cast<const float4*>(im2);
+  const float4* const i1 = reinterpret_cast<const float4*>(im1);
+  // two pixels per iteration with every load issued ahead of the stores (see k_mc_assemble_q);
+  // the flow upsample is up_sample4's arithmetic with unconditional (clamped: i1 == i0 at the
+  // edge, same address) loads
+  auto up = [&](unsigned b, int y, int x) -> float4 {
+    if (!flow_prev) return make_float4(0.f, 0.f, 0.f, 0.f);
+    const UpIdx uy = up_index(y, h, H, 0), ux = up_index(x, w, W, 0);
+    const unsigned bb = b * (unsigned)h * (unsigned)w;
+    const float4 a = f4[bb + (unsigned)uy.i0 * w + ux.i0], bq = f4[bb + (unsigned)uy.i0 * w + ux.i1];
+    const float4 c = f4[bb + (unsigned)uy.i1 * w + ux.i0], d = f4[bb + (unsigned)uy.i1 * w + ux.i1];
+    float4 o;
+    o.x = (a.x * ux.l0 + bq.x * ux.l1) * uy.l0 + (c.x * ux.l0 + d.x * ux.l1) * uy.l1;
+    o.y = (a.y * ux.l0 + bq.y * ux.l1) * uy.l0 + (c.y * ux.l0 + d.y * ux.l1) * uy.l1;
+    o.x = o.x * 2.f;
+    o.y = o.y * 2.f;
+    o.z = 0.f;
+    o.w = 0.f;
+    return o;
+  };
+  for (unsigned p = blockIdx.x * blockDim.x + threadIdx.x; p < npix; p += 2 * st) {
+    const unsigned p2 = p + st < npix ? p + st : p;
+    const unsigned row1 = udiv_magic(p, W, mW), b1 = udiv_magic(row1, H, mH);
+    const unsigned row2 = udiv_magic(p2, W, mW), b2 = udiv_magic(row2, H, mH);
+    const int y1 = (int)(row1 - b1 * H), x1 = (int)(p - row1 * W);
+    const int y2 = (int)(row2 - b2 * H), x2 = (int)(p2 - row2 * W);
+    const float4 a1 = i1[p], a2 = i1[p2];
+    const float4 fu1 = up(b1, y1, x1), fu2 = up(b2, y2, x2);
+    const WarpTap t1 = warp_tap(y1, x1, fu1.x, fu1.y, H, W);
+    const WarpTap t2 = warp_tap(y2, x2, fu2.x, fu2.y, H, W);
+    const float4 wv1 = warp_sample4_nb(i2, b1 * H * W, W, H, t1);
+    const float4 wv2 = warp_sample4_nb(i2, b2 * H * W, W, H, t2);
+    float4* const fo = reinterpret_cast<float4*>(flow_up);
+    float4* const o = reinterpret_cast<float4*>(x8);
+    fo[p] = fu1;
+    o[2 * p] = make_float4(a1.x, a1.y, a1.z, wv1.x);
+    o[2 * p + 1] = make_float4(wv1.y, wv1.z, fu1.x, fu1.y);
+    fo[p2] = fu2;
+    o[2 * p2] = make_float4(a2.x, a2.y, a2.z, wv2.x);
+    o[2 * p2 + 1] = make_float4(wv2.y, wv2.z, fu2.x, fu2.y);
   }
 }
 
 // motion compensation input: warpframe = warp(ref, mv); x8 = [warpframe, ref, 0, 0]
+__device__ __forceinline__ void mc_assemble_px(const float* __restrict__ ref, const float* __restrict__ mv,
+                                               float* __restrict__ warpframe, float* __restrict__ x8, size_t p,
+                                               int x, int y, size_t b, int H, int W) {
+  const float4 f = reinterpret_cast<const float4*>(mv)[p];
+  const WarpTap t = warp_tap(y, x, f.x, f.y, H, W);
+  float4 wv = warp_sample4(ref, b * H * W, W, 1, 0, t);
+  wv.w = 0.f;
+  reinterpret_cast<float4*>(warpframe)[p] = wv;
+  const float4 r = reinterpret_cast<const float4*>(ref)[p];
+  float4* o = reinterpret_cast<float4*>(x8) + p * 2;
+  o[0] = make_float4(wv.x, wv.y, wv.z, r.x);
+  o[1] = make_float4(r.y, r.z, 0.f, 0.f);
+}
+
 __global__ void k_mc_assemble(const float* __restrict__ ref, const float* __restrict__ mv,
                               float* __restrict__ warpframe, float* __restrict__ x8, int B, int H, int W) {
   const size_t npix = (size_t)B * H * W;
-  for (size_t p = grid_stride_start(); p < npix; p += (size_t)gridDim.x * blockDim.x) {
-    const int x = p % W;
-    const int y = (p / W) % H;
-    const size_t b = p / ((size_t)H * W);
-    const float4 f = reinterpret_cast<const float4*>(mv)[p];
-    const WarpTap t = warp_tap(y, x, f.x, f.y, H, W);
-    float4 wv = warp_sample4(ref, b * H * W, W, 1, 0, t);
-    wv.w = 0.f;
-    reinterpret_cast<float4*>(warpframe)[p] = wv;
-    const float4 r = reinterpret_cast<const float4*>(ref)[p];
-    float4* o = reinterpret_cast<float4*>(x8) + p * 2;
-    o[0] = make_float4(wv.x, wv.y, wv.z, r.x);
-    o[1] = make_float4(r.y, r.z, 0.f, 0.f);
+  for (size_t p = grid_stride_start(); p < npix; p += (size_t)gridDim.x * blockDim.x)
+    mc_assemble_px(ref, mv, warpframe, x8, p, p % W, (p / W) % H, p / ((size_t)H * W), H, W);
+}
+
+__global__ void k_mc_assemble_q(const float* __restrict__ ref, const float* __restrict__ mv,
+                                float* __restrict__ warpframe, float* __restrict__ x8, int B, int H, int W,
+                                unsigned mW, unsigned mH) {
+  const unsigned npix = (unsigned)B * H * W;
+  const unsigned st = gridDim.x * blockDim.x;
+  const float4* const r4 = reinterpret_cast<const float4*>(ref);
+  // two pixels per iteration, all loads of both issued before either's stores: the gathers depend
+  // on the flow load (two dependent HBM round trips per pixel), so latency, not bytes, bounds a
+  // one-pixel loop
+  for (unsigned p = blockIdx.x * blockDim.x + threadIdx.x; p < npix; p += 2 * st) {
+    const unsigned p2 = p + st < npix ? p + st : p;
+    const float4 f1 = reinterpret_cast<const float4*>(mv)[p];
+    const float4 f2 = reinterpret_cast<const float4*>(mv)[p2];
+    const float4 r1 = r4[p], r2 = r4[p2];
+    const unsigned row1 = udiv_magic(p, W, mW), b1 = udiv_magic(row1, H, mH);
+    const unsigned row2 = udiv_magic(p2, W, mW), b2 = udiv_magic(row2, H, mH);
+    const WarpTap t1 = warp_tap((int)(row1 - b1 * H), (int)(p - row1 * W), f1.x, f1.y, H, W);
+    const WarpTap t2 = warp_tap((int)(row2 - b2 * H), (int)(p2 - row2 * W), f2.x, f2.y, H, W);
+    float4 w1 = warp_sample4_nb(r4, b1 * H * W, W, H, t1);
+    float4 w2 = warp_sample4_nb(r4, b2 * H * W, W, H, t2);
+    w1.w = 0.f;
+    w2.w = 0.f;
+    float4* const wf = reinterpret_cast<float4*>(warpframe);
+    float4* const o = reinterpret_cast<float4*>(x8);
+    wf[p] = w1;
+    o[2 * p] = make_float4(w1.x, w1.y, w1.z, r1.x);
+    o[2 * p + 1] = make_float4(r1.y, r1.z, 0.f, 0.f);
+    wf[p2] = w2;
+    o[2 * p2] = make_float4(w2.x, w2.y, w2.z, r2.x);
+    o[2 * p2 + 1] = make_float4(r2.y, r2.z, 0.f, 0.f);
   }
 }
 
@@ -1227,8 +1336,14 @@ int fvc_spynet_assemble(const float* im1, const float* im2, const float* flow_pr
                         int batch, int h, int w, fvc_stream_t s) {
   if (!im1 || !im2 || !flow_up || !x8 || (h & 1) || (w & 1) || h < 2 || w < 2) return FVC_EINVAL;
   const size_t n = (size_t)batch * h * w;
-  hipLaunchKernelGGL(k_spynet_assemble, dim3(grid_for(n)), dim3(kBlk), 0, (hipStream_t)s, im1, im2, flow_prev,
-                     flow_up, x8, batch, h, w);
+  if (2ull * n < (1ull << 32) && env_flag("FVC_ASSEMBLE_Q", 1)) {
+    const unsigned mW = (unsigned)(((1ull << 32) + w - 1) / w), mH = (unsigned)(((1ull << 32) + h - 1) / h);
+    hipLaunchKernelGGL(k_spynet_assemble_q, dim3(grid_for(n)), dim3(kBlk), 0, (hipStream_t)s, im1, im2, flow_prev,
+                       flow_up, x8, batch, h, w, mW, mH);
+  } else {
+    hipLaunchKernelGGL(k_spynet_assemble, dim3(grid_for(n)), dim3(kBlk), 0, (hipStream_t)s, im1, im2, flow_prev,
+                       flow_up, x8, batch, h, w);
+  }
   FVC_CHECK_LAUNCH();
   return 0;
 }
@@ -1237,8 +1352,14 @@ int fvc_mc_assemble(const float* ref, const float* mv, float* warpframe, float* 
                     fvc_stream_t s) {
   if (!ref || !mv || !warpframe || !x8 || h < 2 || w < 2) return FVC_EINVAL;
   const size_t n = (size_t)batch * h * w;
-  hipLaunchKernelGGL(k_mc_assemble, dim3(grid_for(n)), dim3(kBlk), 0, (hipStream_t)s, ref, mv, warpframe, x8,
-                     batch, h, w);
+  if (2ull * n < (1ull << 32) && env_flag("FVC_ASSEMBLE_Q", 1)) {
+    const unsigned mW = (unsigned)(((1ull << 32) + w - 1) / w), mH = (unsigned)(((1ull << 32) + h - 1) / h);
+    hipLaunchKernelGGL(k_mc_assemble_q, dim3(grid_for(n)), dim3(kBlk), 0, (hipStream_t)s, ref, mv, warpframe, x8,
+                       batch, h, w, mW, mH);
+  } else {
+    hipLaunchKernelGGL(k_mc_assemble, dim3(grid_for(n)), dim3(kBlk), 0, (hipStream_t)s, ref, mv, warpframe, x8,
+                       batch, h, w);
+  }
   FVC_CHECK_LAUNCH();
   return 0;
 }

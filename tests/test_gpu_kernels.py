@@ -436,6 +436,27 @@ def test_spynet_assemble(dev):
     close(from_nhwc(fu.cpu(), 2), fup, 1e-6)
 
 
+@pytest.mark.parametrize("shape", [(1, 32, 48), (3, 18, 26), (2, 2, 2)])
+def test_assemble_q_forms_bitexact(dev, shape, monkeypatch):
+    """The 32-bit, two-pixels-per-iteration SpyNet / MC assembly kernels (FVC_ASSEMBLE_Q=1, the
+    default: magic-number pixel division, branch-free clamped taps) equal the 64-bit kernels bit
+    for bit, with flows large enough that most taps clamp at the border (odd pixel counts leave
+    one thread a single pixel)."""
+    B, H, W = shape
+    g = torch.Generator().manual_seed(11)
+    im1 = to_nhwc(torch.rand(B, 3, H, W, generator=g)).to(dev)
+    im2 = to_nhwc(torch.rand(B, 3, H, W, generator=g)).to(dev)
+    fprev = to_nhwc(torch.randn(B, 2, H // 2, W // 2, generator=g) * 3 * W).to(dev)
+    mv = to_nhwc(torch.randn(B, 2, H, W, generator=g) * 2 * W).to(dev)
+    outs = []
+    for form in ("0", "1"):
+        monkeypatch.setenv("FVC_ASSEMBLE_Q", form)
+        outs.append(K.spynet_assemble(im1, im2, fprev) + K.mc_assemble(im1, mv) + K.spynet_assemble(im1, im2, None))
+    torch.cuda.synchronize()
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("inverse", [False, True])
 def test_gdn(dev, seeded_sd, inverse):
     from fastvideocodec_amd.net import _GDNP
