@@ -96,6 +96,40 @@ __global__ __launch_bounds__(256) void k_tap_gather(const float* __restrict__ P,
   }
 }
 
+// Stage an IR x IC pixel window of P (c4n float4 per pixel, origin (r0, c0), zeros outside the
+// image) into LDS at pixel stride ps: eight loads per thread in flight per batch, every address
+// clamped into the image and out-of-image values selected to zero after the load (a per-element
+// branch made each load wait for the previous one's LDS write: one HBM round trip per element)
+__device__ __forceinline__ void stage_p_window(const float* __restrict__ Pb, int pcp, int H, int W, int r0, int c0,
+                                               int IR, int IC, int ps, float* sp) {
+  constexpr int NB = 8;
+  const int c4n = pcp >> 2;
+  const int total = IR * IC * c4n;
+  for (int e0 = threadIdx.x; e0 < total; e0 += NB * blockDim.x) {
+    float4 v[NB];
+    int dst[NB];
+#pragma unroll
+    for (int k = 0; k < NB; ++k) {
+      const int e = e0 + k * blockDim.x;
+      const int ee = e < total ? e : total - 1;
+      const int c4 = ee % c4n, p = ee / c4n;
+      const int iy = r0 + p / IC, ix = c0 + p % IC;
+      const bool ok = (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
+      const int cy = min(max(iy, 0), H - 1), cx = min(max(ix, 0), W - 1);
+      const float4 t = *reinterpret_cast<const float4*>(Pb + ((size_t)cy * W + cx) * pcp + 4 * c4);
+      v[k] = ok ? t : make_float4(0.f, 0.f, 0.f, 0.f);
+      dst[k] = e < total ? p * ps + 4 * c4 : -1;
+    }
+#pragma unroll
+    for (int k = 0; k < NB; ++k) {
+      if (dst[k] >= 0) {
+        float* d = sp + dst[k];
+        d[0] = v[k].x; d[1] = v[k].y; d[2] = v[k].z; d[3] = v[k].w;
+      }
+    }
+  }
+}
+
 // Stride-1 3x3 tap gather through LDS (the second half of the fused producer + tap path): a block
 // stages the P tile of its 16 x 32 outputs plus a 1-pixel halo with coalesced 16-B loads (zeros
 // outside the image), pixel stride pcp + 1 words so the per-tap reads of consecutive outputs hit
@@ -108,20 +142,10 @@ __global__ __launch_bounds__(256) void k_tap_gather3_lds(const float* __restrict
   constexpr int TW = 32, IR = TH + 2, IC = TW + 2;
   extern __shared__ float sp[];
   const int ps = pcp + 1;
-  const int c4n = pcp >> 2;
   const size_t b = blockIdx.z;
   const int y0 = blockIdx.y * TH, x0 = blockIdx.x * TW;
   const float* Pb = P + b * H * W * pcp;
-#pragma unroll 4
-  for (int e = threadIdx.x; e < IR * IC * c4n; e += blockDim.x) {
-    const int c4 = e % c4n, p = e / c4n;
-    const int iy = y0 - 1 + p / IC, ix = x0 - 1 + p % IC;
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if ((unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W)
-      v = *reinterpret_cast<const float4*>(Pb + ((size_t)iy * W + ix) * pcp + 4 * c4);
-    float* d = sp + p * ps + 4 * c4;
-    d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
-  }
+  stage_p_window(Pb, pcp, H, W, y0 - 1, x0 - 1, IR, IC, ps, sp);
   __syncthreads();
   for (int q = threadIdx.x; q < TH * TW; q += blockDim.x) {
     const int r = q / TW, c = q % TW;
@@ -168,21 +192,12 @@ __global__ __launch_bounds__(256) void k_tap_gather_t2_lds(const float* __restri
   constexpr int TW = 32, IR = TH / 2 + 2, IC = 19, pad = KS / 2;
   extern __shared__ float sp[];
   const int ps = pcp + 1;
-  const int c4n = pcp >> 2;
   const int Ho = 2 * H, Wo = 2 * W;
   const size_t b = blockIdx.z;
   const int Y0 = blockIdx.y * TH, X0 = blockIdx.x * TW;
   const int r0 = Y0 / 2 - 1, c0 = X0 / 2 - 1;
   const float* Pb = P + b * H * W * pcp;
-  for (int e = threadIdx.x; e < IR * IC * c4n; e += blockDim.x) {
-    const int c4 = e % c4n, p = e / c4n;
-    const int iy = r0 + p / IC, ix = c0 + p % IC;
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if ((unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W)
-      v = *reinterpret_cast<const float4*>(Pb + ((size_t)iy * W + ix) * pcp + 4 * c4);
-    float* d = sp + p * ps + 4 * c4;
-    d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
-  }
+  stage_p_window(Pb, pcp, H, W, r0, c0, IR, IC, ps, sp);
   __syncthreads();
   for (int q = threadIdx.x; q < TH * TW; q += blockDim.x) {
     const int Y = Y0 + q / TW, X = X0 + q % TW;

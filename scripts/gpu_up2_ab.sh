@@ -1,5 +1,5 @@
 #!/bin/bash
-# upsample-add two elements per iteration (product libfvc.so) vs the one-element form (experiment
+# product libfvc.so vs the previous commit's library (experiment
 # library libfvc_wold.so from the previous commit): kernel tests, then the bench's serial HBM timings
 export TMPDIR=/tmp
 OUT=gpurun_out/up2ab; mkdir -p $OUT
@@ -12,5 +12,5 @@ for rep in 1 2; do for v in old new; do
     --json-out $OUT/b_${v}_$rep.json > $OUT/b_${v}_$rep.log 2>&1 || { tail -20 $OUT/b_${v}_$rep.log; exit 1; }
   python -c "
 import json; d=json.load(open('$OUT/b_${v}_$rep.json')); h=d['hbm_kernels']
-print('$v rep $rep', d['value'], {k: (h[k]['ms_per_pframe'], h[k]['gb_per_s']) for k in ('upsample2x_add', 'mc_assemble (warp)')})"
+print('$v rep $rep', d['value'], {k: (h[k]['ms_per_pframe'], h[k]['gb_per_s']) for k in ('tap_gather', 'gdn+tap', 'upsample2x_add')})"
 done; done
