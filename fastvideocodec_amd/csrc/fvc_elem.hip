@@ -449,6 +449,23 @@ __global__ void k_up2_add(const float* __restrict__ src, const float* __restrict
   }
 }
 
+// 4-channel form of k_nchw_to_nhwc (frames and flows: C <= 4 into a 4-channel pixel): one 16-B
+// store per pixel instead of four 4-B ones, the image split by a multiply-high division
+__global__ void k_nchw_to_nhwc4(const float* __restrict__ src, float* __restrict__ dst, int B, int C,
+                                unsigned HW, unsigned mHW) {
+  const unsigned npix = (unsigned)B * HW;
+  for (unsigned p = blockIdx.x * blockDim.x + threadIdx.x; p < npix; p += gridDim.x * blockDim.x) {
+    const unsigned b = udiv_magic(p, HW, mHW);
+    const float* const sp = src + (size_t)b * C * HW + (p - b * HW);
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (C > 0) v.x = sp[0];
+    if (C > 1) v.y = sp[HW];
+    if (C > 2) v.z = sp[2 * (size_t)HW];
+    if (C > 3) v.w = sp[3 * (size_t)HW];
+    reinterpret_cast<float4*>(dst)[p] = v;
+  }
+}
+
 // ------------------------------------------------------------------ SpyNet level assembly
 __device__ __forceinline__ void spynet_assemble_px(const float* __restrict__ im1, const float* __restrict__ im2,
                                                    const float* __restrict__ flow_prev, float* __restrict__ flow_up,
@@ -1299,7 +1316,15 @@ int fvc_device_arch_ok(void) {
 int fvc_nchw_to_nhwc(const float* src, float* dst, int batch, int c, int h, int w, int cp, fvc_stream_t s) {
   if (!src || !dst || c > cp || cp % 4) return FVC_EINVAL;
   const size_t n = (size_t)batch * h * w;
-  hipLaunchKernelGGL(k_nchw_to_nhwc, dim3(grid_for(n)), dim3(kBlk), 0, (hipStream_t)s, src, dst, batch, c, h, w, cp);
+  const unsigned long long hw = (unsigned long long)h * w;
+  if (cp == 4 && hw >= 2 && 2ull * n < (1ull << 32)) {
+    const unsigned m = (unsigned)(((1ull << 32) + hw - 1) / hw);
+    hipLaunchKernelGGL(k_nchw_to_nhwc4, dim3(grid_for(n)), dim3(kBlk), 0, (hipStream_t)s, src, dst, batch, c,
+                       (unsigned)hw, m);
+  } else {
+    hipLaunchKernelGGL(k_nchw_to_nhwc, dim3(grid_for(n)), dim3(kBlk), 0, (hipStream_t)s, src, dst, batch, c, h, w,
+                       cp);
+  }
   FVC_CHECK_LAUNCH();
   return 0;
 }

@@ -408,6 +408,19 @@ def test_upsample_64ch_forms_bit_identical(dev, shape, with_skip, monkeypatch):
     close(from_nhwc(outs[0].cpu(), 64), ref, 1e-6)
 
 
+@pytest.mark.parametrize("shape", [(2, 3, 17, 29), (1, 2, 64, 96), (3, 1, 5, 3), (1, 4, 2, 1), (1, 6, 8, 8)])
+def test_nchw_to_nhwc(dev, shape):
+    """The boundary layout conversion: NCHW -> NHWC padded to a multiple of 4 channels (pad = 0);
+    C <= 4 into 4 channels takes the 16-B-store kernel (k_nchw_to_nhwc4), the rest the generic one."""
+    x = torch.randn(*shape)
+    y = K.nchw_to_nhwc(x.to(dev)).cpu()
+    B, C, H, W = shape
+    cp = (C + 3) // 4 * 4
+    ref = torch.zeros(B, H, W, cp)
+    ref[..., :C] = x.permute(0, 2, 3, 1)
+    assert torch.equal(y, ref)
+
+
 def test_avgpool(dev):
     x = torch.randn(2, 64, 18, 34)
     y = K.avgpool2(to_nhwc(x).to(dev))
