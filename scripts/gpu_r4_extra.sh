@@ -10,6 +10,7 @@ run() {  # tag timeout args...
   python -c "import json; d=json.load(open('$OUT/$tag.json')); print('$tag', d['value'], d['unit'], d['ms_per_step'])"
 }
 run tree 400 --tree --steps 3 --warmup 1 && \
+run tree8 400 --tree --gops-per-gpu 8 --steps 3 --warmup 1 && \
 run views8 400 --views 8 --steps 3 --warmup 1 && \
 run k4_gop32 500 --height 2160 --width 3840 --gop 32 --gops-per-gpu 1 --steps 2 --warmup 1 || exit 1
 # two RCCL ranks sharing the box's one GPU (a probe: RCCL may refuse a duplicate device)
