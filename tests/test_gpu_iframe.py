@@ -95,3 +95,25 @@ def test_container_roundtrip_gop_view_muxing(model, dev):
     other = get_codec_model("DVC-pretrained", compression_level=2, device=dev, seed=7)
     with pytest.raises(ValueError):
         CT.decode_video(other, data)
+
+
+@pytest.mark.parametrize("framing", ["segment", "channel", "item"])
+def test_container_roundtrip_each_framing(model, dev, framing):
+    """Every P-frame stream framing through the container (framing code 0 channel, 1 item,
+    2 segment) at 512x512, where the 1024-symbol mv / feature rows really are cut in two
+    segments: the decoder reproduces the encoder's reconstructions bit for bit and the record
+    holds the framing's stream count."""
+    from fastvideocodec_amd.net import FRAMINGS, stream_rows
+    video = torch.from_numpy(np.stack([make_gop(512, 512, 3, 90)])).to(dev)
+    buf = io.BytesIO()
+    rec = CT.encode_video(model, video, buf, framing=framing)
+    data = buf.getvalue()
+    dec = CT.decode_video(model, data)
+    torch.cuda.synchronize()
+    assert torch.equal(dec[(0, 0)], rec[0])
+    r = CT.ContainerReader(data)
+    payload = r.record(r.gop_records(0, 0)[1])
+    assert payload[1] == FRAMINGS.index(framing)
+    n_mv = int.from_bytes(payload[10:14], "little")  # streams(mv) count after the 10-byte head
+    assert n_mv == stream_rows(framing, 1, 128, 32 * 32)[0]
+
