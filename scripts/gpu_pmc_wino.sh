@@ -3,7 +3,7 @@
 # per rocprofv3 run under `timeout -s KILL`; then the same for the direct kernel (FVC_WINO=0).
 export TMPDIR=/tmp
 CASE=${CASE:-c3_64_full}
-for V in 1 0; do
+for V in ${VS:-1 0}; do
 OUT=gpurun_out/pmcw${V}_$CASE; mkdir -p $OUT
 pass() {
   local name=$1; shift
