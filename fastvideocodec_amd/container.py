@@ -43,7 +43,11 @@ _IDX = struct.Struct("<cHIHQ")
 def tables_crc(model) -> str:
     """CRC-32 over the model's quantised CDF tables (mv, z, feature) and scale table."""
     model.update()
-    tz, tmv, tf = model._coders["tables"]
+    return tables_crc_of(*model._coders["tables"])
+
+
+def tables_crc_of(tz, tmv, tf) -> str:
+    """tables_crc of host tables (FactorizedTables z / mv, LaplaceTables feature)."""
     c = 0
     for t in (tmv, tz, tf):
         for a in (t.cdf, t.cdf_length, t.offset):

@@ -1377,8 +1377,9 @@ int fvc_spynet_assemble(const float* im1, const float* im2, const float* flow_pr
   if (!im1 || !im2 || !flow_up || !x8 || (h & 1) || (w & 1) || h < 2 || w < 2) return FVC_EINVAL;
   const size_t n = (size_t)batch * h * w;
   if (2ull * n < (1ull << 32) && env_flag("FVC_ASSEMBLE_Q", 1)) {
+    // two pixels per thread per iteration: half as many threads as pixels
     const unsigned mW = (unsigned)(((1ull << 32) + w - 1) / w), mH = (unsigned)(((1ull << 32) + h - 1) / h);
-    hipLaunchKernelGGL(k_spynet_assemble_q, dim3(grid_for(n)), dim3(kBlk), 0, (hipStream_t)s, im1, im2, flow_prev,
+    hipLaunchKernelGGL(k_spynet_assemble_q, dim3(grid_for((n + 1) / 2)), dim3(kBlk), 0, (hipStream_t)s, im1, im2, flow_prev,
                        flow_up, x8, batch, h, w, mW, mH);
   } else {
     hipLaunchKernelGGL(k_spynet_assemble, dim3(grid_for(n)), dim3(kBlk), 0, (hipStream_t)s, im1, im2, flow_prev,
@@ -1394,7 +1395,7 @@ int fvc_mc_assemble(const float* ref, const float* mv, float* warpframe, float* 
   const size_t n = (size_t)batch * h * w;
   if (2ull * n < (1ull << 32) && env_flag("FVC_ASSEMBLE_Q", 1)) {
     const unsigned mW = (unsigned)(((1ull << 32) + w - 1) / w), mH = (unsigned)(((1ull << 32) + h - 1) / h);
-    hipLaunchKernelGGL(k_mc_assemble_q, dim3(grid_for(n)), dim3(kBlk), 0, (hipStream_t)s, ref, mv, warpframe, x8,
+    hipLaunchKernelGGL(k_mc_assemble_q, dim3(grid_for((n + 1) / 2)), dim3(kBlk), 0, (hipStream_t)s, ref, mv, warpframe, x8,
                        batch, h, w, mW, mH);
   } else {
     hipLaunchKernelGGL(k_mc_assemble, dim3(grid_for(n)), dim3(kBlk), 0, (hipStream_t)s, ref, mv, warpframe, x8,

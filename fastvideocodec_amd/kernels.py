@@ -264,6 +264,18 @@ def x3_dispatches(batch, y_image_bytes, res_image_bytes=0):
     return n(batch)
 
 
+# every environment switch the split-precision conv sources read (fvc_conv_x3.hip, fvc_deconv_x3.hip,
+# fvc_conv_wino.hip): a pack's layout id is re-queried only when one of them changes
+_LAYOUT_ENV = ("FVC_DX", "FVC_DX_PAIR", "FVC_X3_BPC", "FVC_X3_CC", "FVC_X3_CIN4", "FVC_X3_DYN", "FVC_X3_PRIO",
+               "FVC_X3_PT", "FVC_X3_RESERVE", "FVC_X3_SMALLN", "FVC_X3_SPLIT_BYTES", "FVC_X3_WG", "FVC_X3_WL",
+               "FVC_X3_WM", "FVC_X3_WN", "FVC_X3_XCD")
+
+
+def _layout_env():
+    get = os.environ.get
+    return tuple(get(k) for k in _LAYOUT_ENV)
+
+
 class PackedConv:
     """A conv / transposed conv with weights packed once for its HIP kernel: the split-precision
     fp16 x3 kernel where supported (cin padded to a multiple of 8, cout > 4), else fp32 MFMA /
@@ -340,9 +352,15 @@ class PackedConv:
 
     def _check_layout(self):
         """The pack's layout must be the one the launch will assume: FVC_DX / FVC_X3_PT / FVC_X3_CIN4 /
-        FVC_X3_CC / FVC_X3_SMALLN are read by the C side at pack and at launch."""
+        FVC_X3_CC / FVC_X3_SMALLN are read by the C side at pack and at launch. The C
+        query rebuilds the tap tables, so it runs again only when one of the switches the conv
+        sources read has changed since this pack was last checked."""
+        env = _layout_env()
+        if env == getattr(self, "_layout_env", None):
+            return
         now = int(_lib.load().fvc_conv_x3_layout_id(self.cin, self.cout, self.ksize, self.stride,
                                                       int(self.transposed)))
+        self._layout_env = env
         if now != self.layout:
             raise _lib.FvcError("x3 weight pack was built under another layout configuration (an FVC_DX / "
                                 "FVC_X3_* switch changed since packing); re-create the PackedConv")

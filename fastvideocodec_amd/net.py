@@ -378,6 +378,21 @@ def stream_rows(framing: str, B: int, C: int, hw: int):
     return B * C, hw
 
 
+def bitstream_rows(framing: str, B: int, C: int, hw: int, nstreams: int):
+    """(streams, symbols per stream) of a coded [B, C, hw] latent, read from the stream count the
+    bitstream carries rather than re-derived from SEGMENT_MIN / segments(): a file written under
+    another segmenting rule still decodes, and a count that cannot cut the rows is rejected."""
+    if framing == "segment":
+        s = nstreams // max(B * C, 1)
+        if s < 1 or s * B * C != nstreams or hw % s:
+            raise FvcError(f"segment framing: {nstreams} streams cannot cut {B * C} rows of {hw} symbols")
+        return nstreams, hw // s
+    rows = stream_rows(framing, B, C, hw)
+    if rows[0] != nstreams:
+        raise FvcError(f"{framing} framing: expected {rows[0]} streams, bitstream has {nstreams}")
+    return rows
+
+
 class PFrameBitstream:
     """In-memory P-frame bitstream: three latents (mv, z, feature) of ``batch`` frames.
 
@@ -610,20 +625,20 @@ class VideoCompressor(nn.Module):
         B = bs.batch
         (H16, W16), (H64, W64) = bs.hw16, bs.hw64
         dev = bs.mv.packed.device
-        rows = lambda C, hw: stream_rows(bs.framing, B, C, hw)  # noqa: E731
+        rows = lambda C, hw, part: bitstream_rows(bs.framing, B, C, hw, part.nstreams)  # noqa: E731
         # stream checks are collected on the device and read once at the end (one host wait per
         # frame instead of two per latent)
         st = [] if check else None
         with torch.no_grad(), K.precision(bs.precision):
             idx_z = K.channel_indexes(B, H64 * W64, OUT_CHANNEL_N, dev)
-            sym_z = c["z"].decode(bs.z, idx_z.view(rows(OUT_CHANNEL_N, H64 * W64)), check, st).view(B, OUT_CHANNEL_N, H64 * W64)
+            sym_z = c["z"].decode(bs.z, idx_z.view(rows(OUT_CHANNEL_N, H64 * W64, bs.z)), check, st).view(B, OUT_CHANNEL_N, H64 * W64)
             z = K.symbols_to_latent(sym_z, H64, W64, OUT_CHANNEL_N)
             sigma = self.respriorDecoder.run(z)
             idx_f = K.build_indexes(sigma, c["scale_table"], OUT_CHANNEL_M)
-            sym_f = c["feature"].decode(bs.feature, idx_f.view(rows(OUT_CHANNEL_M, H16 * W16)), check, st).view(B, OUT_CHANNEL_M, H16 * W16)
+            sym_f = c["feature"].decode(bs.feature, idx_f.view(rows(OUT_CHANNEL_M, H16 * W16, bs.feature)), check, st).view(B, OUT_CHANNEL_M, H16 * W16)
             feature = K.symbols_to_latent(sym_f, H16, W16, OUT_CHANNEL_M)
             idx_mv = K.channel_indexes(B, H16 * W16, OUT_CHANNEL_MV, dev)
-            sym_mv = c["mv"].decode(bs.mv, idx_mv.view(rows(OUT_CHANNEL_MV, H16 * W16)), check, st).view(B, OUT_CHANNEL_MV, H16 * W16)
+            sym_mv = c["mv"].decode(bs.mv, idx_mv.view(rows(OUT_CHANNEL_MV, H16 * W16, bs.mv)), check, st).view(B, OUT_CHANNEL_MV, H16 * W16)
             mvq = K.symbols_to_latent(sym_mv, H16, W16, OUT_CHANNEL_MV)
         if st and int(torch.cat(st).abs().max()) != 0:
             raise FvcError("corrupt rANS stream (or a failed encode)")

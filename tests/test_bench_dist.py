@@ -138,6 +138,20 @@ def test_bench_views8_gpus8_view_v_on_rank_v(tmp_path):
     assert res["n_gpus"] == 8 and res["config"]["parallelism"] == "view-shard x8"
     assert res["shards"] == {"unit": "view", "by_rank": [[v] for v in range(8)]}
     assert res["config"]["views_per_gpu"] == 1
+    # at N = 8 only ranks 0..3 (--parity-ranks default) run the oracle parity check
+    pa = res["quality"]["parity_all_ranks"]
+    assert pa["ranks_checked"] == 4 and pa["parity_ranks_cap"] == 4 and "ranks 0..3" in pa["note"]
+    assert pa["ok"] is True
+    pr = res["quality"]["parity_by_rank"]
+    assert [p.get("checked", True) for p in pr] == [True] * 4 + [False] * 4
+
+
+def test_bench_parity_ranks_flag_and_strict(tmp_path):
+    """--parity-ranks 1 at N = 2 checks rank 0 only; --strict-parity exits 0 when parity holds."""
+    res = _run_bench_cli(["--gpus", "2", "--steps", "1", "--warmup", "0", "--gops-per-gpu", "1", "--height", "64",
+                          "--width", "128", "--gop", "3", "--parity-ranks", "1", "--strict-parity"], tmp_path)
+    pa = res["quality"]["parity_all_ranks"]
+    assert pa["ranks_checked"] == 1 and pa["ok"] is True
 
 
 def test_bench_refuses_gpus_mismatch_under_launcher(monkeypatch):

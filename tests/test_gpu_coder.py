@@ -274,3 +274,30 @@ def test_overflow_flag_is_stream_local(dev):
         pc(x)
         assert K.x3_overflow(reset=True)
     assert not K.x3_overflow(reset=True)
+
+
+def test_segment_framed_container_fixture_decodes(model, dev):
+    """the committed segment-framed container (written on CPU by the C oracle coder,
+    tests/golden/gen_container_fixture.py) decodes on the device: the entropy decode gives the
+    committed symbols exactly, and the reconstruction matches the oracle decoder's PSNR."""
+    import os
+
+    from fastvideocodec_amd import container as CT
+    from fastvideocodec_amd.synthetic import make_gop
+
+    base = os.path.join(os.path.dirname(__file__), "golden", "pframe_segment_256x1024")
+    g = np.load(base + ".npz")
+    with open(base + ".fvc", "rb") as f:
+        r = CT.ContainerReader(f.read())
+    assert r.header["tables_crc32"] == CT.tables_crc(model)
+    bs = CT.pframe_from_payload(r.record(r.index[0]), dev)
+    assert bs.framing == "segment" and (bs.mv.nstreams, bs.z.nstreams, bs.feature.nstreams) == (256, 64, 192)
+    lat = model.decode_latents(bs)
+    for name, key, C in (("mv", "mv", 128), ("z", "z", 64), ("feature", "feature", 96)):
+        got = K.latent_to_symbols(lat[key], C).cpu().numpy().reshape(C, -1)
+        assert (got == g[f"sym_{name}"].astype(np.int32)).all(), name
+    H, W = int(g["height"]), int(g["width"])
+    frames = make_gop(H, W, 2, int(g["seed"]))
+    rec = model.decompress(bs, torch.from_numpy(frames[0:1].copy()).to(dev)).cpu().numpy().astype(np.float64)
+    psnr = 10 * np.log10(1.0 / np.mean((rec - frames[1:2]) ** 2))
+    assert abs(psnr - float(g["oracle_decode_psnr_db"])) <= 1e-4, (psnr, float(g["oracle_decode_psnr_db"]))

@@ -10,6 +10,7 @@ from fastvideocodec_amd.synthetic import make_gop
 from fastvideocodec_amd.tree_gop import coding_layers, encode_decode_tree_gop
 
 pytestmark = pytest.mark.gpu
+TREE_DRIFT_CAP_DB = 5e-3  # r2's fixed closed-loop cap
 
 
 @pytest.fixture(scope="module")
@@ -104,7 +105,10 @@ def test_tree_gop_vs_oracle(model, dev, seeded_sd):
         drift.append(abs(pd - po))
         drift32.append(abs(p32 - po))
     print("tree closed-loop PSNR drift (dB): x3", np.array(drift), "f32", np.array(drift32))
-    assert max(drift) <= max(2 * max(drift32), 1e-4), (drift, drift32)
+    # the anchored bound keeps the old fixed cap as a ceiling, and the fp32 drift itself
+    # must stay under it (a kernel shared by both precisions cannot loosen the bound)
+    assert max(drift32) <= TREE_DRIFT_CAP_DB, drift32
+    assert max(drift) <= min(max(2 * max(drift32), 1e-4), TREE_DRIFT_CAP_DB), (drift, drift32)
 
 
 def test_tree_gop_streaming_join_false(model, dev):
