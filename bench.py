@@ -483,7 +483,7 @@ class GpuGopJob:
         r = {"conv": timer.collect(), "x3": timer.collect(x3=True), "x3_bytes": timer.collect_bytes(x3=True),
              "hbm": timer.collect_hbm(),
              "family": {f: (timer.collect(x3=True, family=f), timer.collect_bytes(x3=True, family=f))
-                        for f in ("x3", "dx", "wino")}}
+                        for f in ("x3", "dx", "wino", "wr7")}}
         if self.args.breakdown:
             for k, (n, ms, fl) in sorted(timer.breakdown().items(), key=lambda kv: -kv[1][1]):
                 print(f"{k:40s} n={n:5d} ms={ms:9.2f} TF/s={fl / (ms * 1e-3) / 1e12:7.2f}", file=sys.stderr)
@@ -698,10 +698,12 @@ def roofline_fields(prof, job, args):
                                "conv_x3_kernel (fp16x3 implicit-GEMM conv/deconv) + conv_dx_kernel (stride-2 "
                                "transposed convs, all parity classes per staged tile) + conv_wino_kernel (Winograd "
                                "F(2x2,3x3) for the 64->64 3x3 layers, and the 544x960 128->128 ones as four 64->64 "
-                               "quarters), all their dispatches",
+                               "quarters) + conv_wr7_kernel (Winograd-rows F(2,7) for SpyNet's 7x7 32->64, 64->32 "
+                               "and 32->16 layers), all their dispatches",
                      "achieved_is": "algorithmic fp32-conv FLOP (2 x MAC of the direct convolution) / kernel time; "
                                     "the direct kernel issues 3 f16 MFMAs per MAC (ceiling peak/3), the Winograd "
-                                    "kernel 3 per 16/36 MAC (ceiling peak/3 x 36/16)",
+                                    "kernel 3 per 16/36 MAC (ceiling peak/3 x 36/16), the Winograd-rows kernel 3 per "
+                                    "28/49 MAC (ceiling peak/3 x 49/28)",
                      "x3_ceiling": round(F16_MFMA_PEAK_TFLOPS / 3, 1),
                      "frac_of_x3_ceiling": round(achieved / (F16_MFMA_PEAK_TFLOPS / 3), 4),
                      **issued_fields(prof, x3_ms),
@@ -722,8 +724,9 @@ def roofline_fields(prof, job, args):
 
 
 # f16 MFMA FLOP issued per algorithmic fp32-conv FLOP, per kernel family: 3 split products (hi*hi,
-# hi*lo, lo*hi) per MAC; Winograd F(2x2,3x3) computes 16 products per 36 direct MACs
-ISSUED_PER_FLOP = {"x3": 3.0, "dx": 3.0, "wino": 3.0 * 16.0 / 36.0}
+# hi*lo, lo*hi) per MAC; Winograd F(2x2,3x3) computes 16 products per 36 direct MACs, the
+# Winograd-rows F(2,7) 28 per 49
+ISSUED_PER_FLOP = {"x3": 3.0, "dx": 3.0, "wino": 3.0 * 16.0 / 36.0, "wr7": 3.0 * 28.0 / 49.0}
 
 
 def issued_fields(prof, fam_ms):
@@ -750,7 +753,8 @@ def per_kernel_fields(prof, nfr):
     conv_dx_kernel and conv_wino_kernel, and for Winograd the f16 matrix rate it actually issues (3 MFMAs per
     16/36 of a direct MAC)."""
     out = {}
-    for fam, name in (("x3", "conv_x3_kernel"), ("dx", "conv_dx_kernel"), ("wino", "conv_wino_kernel")):
+    for fam, name in (("x3", "conv_x3_kernel"), ("dx", "conv_dx_kernel"), ("wino", "conv_wino_kernel"),
+                      ("wr7", "conv_wr7_kernel")):
         (ms, fl, n), nbytes = prof["family"][fam]
         if not n:
             continue

@@ -330,6 +330,22 @@ class PackedConv:
             self.osc4 = (ctypes.c_float * 4)()
             _lib.call("fvc_conv_wino128_pack_weight", w.data_ptr(), q.data_ptr(), ctypes.addressof(self.osc4))
             self.upack128 = q.to(device)
+        # SpyNet's 7x7 stride-1 32->64 / 64->32 / 32->16 layers: Winograd-rows F(2,7) split-precision
+        # kernel (fvc_conv_wr7.hip; 1.75x fewer MFMAs), as launches of 32 input x 16 * nt output
+        # channels: (ci0, co0, nt, mode, upack, osc); a 64-channel input's second half adds the first
+        # half's partial sum (mode 1 then 2). FVC_WR7=0 keeps the direct x3 kernel (A/B, tests).
+        self.wr7 = []
+        if (self.x3 and os.environ.get("FVC_WR7", "1") != "0" and
+                bool(lib.fvc_conv_wr7_supported(cin, cout, ksize, stride, int(transposed)))):
+            nt = 1 if cout == 16 else 2
+            for co0 in range(0, cout, 16 * nt):
+                for ci0 in range(0, cin, 32):
+                    mode = 0 if cin == 32 else (1 if ci0 == 0 else 2)
+                    up = torch.empty(lib.fvc_conv_wr7_wpack_bytes(nt) // 2, dtype=torch.float16)
+                    uo = ctypes.c_float(0.0)
+                    _lib.call("fvc_conv_wr7_pack_weight", w.data_ptr(), cin, cout, ci0, co0, nt, up.data_ptr(),
+                              ctypes.addressof(uo))
+                    self.wr7.append((ci0, co0, nt, mode, up.to(device), float(uo.value)))
         # stride-2 transposed layers on the all-classes kernel (fvc_deconv_x3.hip, conv_dx_kernel)
         self.dx = self.x3 and transposed and bool(lib.fvc_deconv_x3_all_classes(cin, cout, ksize, stride))
         if self.x3:
@@ -401,7 +417,15 @@ class PackedConv:
         # many frames share its batch.
         w128 = (self.wino128 and in_op in (IN_NONE, IN_RELU) and post == POST_NONE and res is None and
                 H * W >= int(os.environ.get("FVC_WINO128_MINPIX", "200000")))
-        if wino:
+        wr7 = bool(self.wr7) and in_op == IN_NONE and post == POST_NONE and res is None
+        if wr7:
+            xp, yp = cp4(self.cin), cp4(self.cout)
+            for ci0, co0, nt, mode, up, uo in self.wr7:
+                _lib.call("fvc_conv2d_nhwc_wr7", x.data_ptr() + 4 * ci0, xp, up.data_ptr(), nt, uo,
+                          self.bias.data_ptr() + 4 * co0, y.data_ptr() + 4 * co0, yp, B, H, W, mode,
+                          ACT_NONE if mode == 1 else act, _STATE["cu_reserve"], overflow_flag(x.device).data_ptr(),
+                          sched_scratch(x.device).data_ptr(), SCHED_LEN, stream_handle())
+        elif wino:
             _lib.call("fvc_conv2d_nhwc_wino", x.data_ptr(), self.upack.data_ptr(), self.uosc, self.bias.data_ptr(),
                       _ptr(res), y.data_ptr(), None, B, H, W, in_op, act, _STATE["cu_reserve"],
                       overflow_flag(x.device).data_ptr(), sched_scratch(x.device).data_ptr(), SCHED_LEN,
@@ -431,10 +455,11 @@ class PackedConv:
             timer.records.append((ev0, ev1, profiling.conv_flops(self.cin, self.cout, self.ksize, self.stride,
                                                                  self.transposed, B, H, W),
                                   f"{'deconv' if self.transposed else 'conv'}{self.ksize}s{self.stride} "
-                                  f"{self.cin}->{self.cout} @{H}x{W}{' wino' if wino else (' dx' if self.dx else (' x3' if self.x3 else ''))}"
-                                  f"{' x4' if w128 else ''}",
-                                  self.x3, nbytes, "wino" if wino else ("dx" if self.dx else ("x3" if self.x3 else "f32")),
-                                  4 if w128 else (1 if wino or not self.x3 else
+                                  f"{self.cin}->{self.cout} @{H}x{W}{' wr7' if wr7 else (' wino' if wino else (' dx' if self.dx else (' x3' if self.x3 else '')))}"
+                                  f"{' x4' if w128 else ''}{f' x{len(self.wr7)}' if wr7 and len(self.wr7) > 1 else ''}",
+                                  self.x3, nbytes,
+                                  "wr7" if wr7 else ("wino" if wino else ("dx" if self.dx else ("x3" if self.x3 else "f32"))),
+                                  len(self.wr7) if wr7 else 4 if w128 else (1 if wino or not self.x3 else
                                                   x3_dispatches(B, 4 * y[0].numel(),
                                                                 4 * res[0].numel() if res is not None else 0))))
         return y

@@ -182,6 +182,23 @@ int fvc_conv2d_nhwc_wino128(const float* x, const void* wpack, const float* osc4
                             float* y, int batch, int h, int w, int in_op, int act, int cu_reserve,
                             int* overflow_flag, int* sched, int sched_len, fvc_stream_t stream);
 
+/* Winograd-rows F(2,7) split-precision conv for SpyNet's 7x7 stride-1 pad-3 layers (MEBasic,
+ * endecoder.py:142-169: conv2 32 -> 64, conv3 64 -> 32, conv4 32 -> 16; replaces the same
+ * torch.nn.Conv2d forwards as fvc_conv2d_nhwc_x3). One launch covers 32 input channels and
+ * 16 * nt (nt 1 or 2) output channels: x points at input channel ci0 (pixel pitch xp floats),
+ * y at output channel co0 (pitch yp), bias at bias + co0. mode 0: y = act(conv + bias); mode 1:
+ * y = conv (first 32-channel input half of a 64-channel layer, bias unused); mode 2:
+ * y = act(conv + bias + y) (the second half). upack: fvc_conv_wr7_wpack_bytes(nt) bytes from
+ * fvc_conv_wr7_pack_weight (host; w OIHW [cout][cin][7][7], the block ci0 .. ci0+31 x
+ * co0 .. co0+16nt-1), osc from the same call. sched: >= 2 ints, zero between launches. */
+int fvc_conv_wr7_supported(int cin, int cout, int ksize, int stride, int transposed);
+size_t fvc_conv_wr7_wpack_bytes(int nt);
+int fvc_conv_wr7_pack_weight(const float* w_host, int cin, int cout, int ci0, int co0, int nt,
+                             void* wpack_host, float* osc_out);
+int fvc_conv2d_nhwc_wr7(const float* x, int xp, const void* upack, int nt, float osc, const float* bias,
+                        float* y, int yp, int batch, int h, int w, int mode, int act, int cu_reserve,
+                        int* overflow_flag, int* sched, int sched_len, fvc_stream_t stream);
+
 /* ------------------------------------------------------------------ layout / resampling */
 int fvc_nchw_to_nhwc(const float* src, float* dst, int batch, int c, int h, int w, int cp,
                      fvc_stream_t stream);

@@ -1,0 +1,135 @@
+"""The Winograd-rows F(2,7) split-precision conv (fvc_conv_wr7.hip, SpyNet's 7x7 layers, MEBasic
+endecoder.py:142-169) against float64 torch convs of the same op and against the direct
+split-precision kernel: the three geometries it takes (32->64 as two output-channel launches,
+64->32 as two input-channel launches with the partial-sum form, 32->16), sizes cut at every edge
+(partial 32-column strips, images shorter than a 128-row work item and crossing it), ReLU / none
+activations, the dynamic and static schedules, determinism and the overflow flag.
+
+Accuracy gate: error against float64 no worse than the direct split kernel's on
+the same layer (CPU emulation predicts equal: scripts/wino_accuracy.py spynet)."""
+import os
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from fastvideocodec_amd import kernels as K
+
+pytestmark = pytest.mark.gpu
+
+
+def to_nhwc(x, cp=None):
+    return x.permute(0, 2, 3, 1).contiguous()
+
+
+def from_nhwc(y, c):
+    return y[..., :c].permute(0, 3, 1, 2).contiguous()
+
+
+def _packs(dev, w, b):
+    """(Winograd-rows, direct x3) packs of the same 7x7 layer."""
+    pw = K.PackedConv(w, b, 7, 1, False, dev, precision="x3")
+    assert pw.wr7
+    old = os.environ.get("FVC_WR7")
+    os.environ["FVC_WR7"] = "0"
+    try:
+        pd = K.PackedConv(w, b, 7, 1, False, dev, precision="x3")
+    finally:
+        if old is None:
+            del os.environ["FVC_WR7"]
+        else:
+            os.environ["FVC_WR7"] = old
+    assert not pd.wr7 and pd.x3
+    return pw, pd
+
+
+# (cin, cout, B, H, W, relu)
+CASES = [
+    (32, 64, 1, 40, 72, True),     # conv2; partial last column strip
+    (64, 32, 2, 37, 70, True),     # conv3 (two input halves); odd height
+    (32, 16, 1, 8, 30, True),      # conv4; one strip narrower than 32 columns
+    (32, 64, 1, 136, 240, True),   # SpyNet level /8 size
+    (64, 32, 1, 300, 64, False),   # three 128-row work items per column, no activation
+    (32, 16, 3, 129, 97, False),   # crosses one work item by a row; ragged width
+]
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_wr7_vs_float64_and_direct(dev, case):
+    cin, cout, B, H, W, relu = case
+    g = torch.Generator().manual_seed(7 * H + W)
+    x = torch.relu(torch.randn(B, cin, H, W, generator=g))  # SpyNet's layer inputs are ReLU outputs
+    w = torch.randn(cout, cin, 7, 7, generator=g) * (1.0 / (cin * 49) ** 0.5)
+    b = torch.randn(cout, generator=g) * 0.1
+    ref = F.conv2d(x.double(), w.double(), b.double(), 1, 3)
+    if relu:
+        ref = torch.relu(ref)
+    pw, pd = _packs(dev, w, b)
+    act = K.ACT_RELU if relu else K.ACT_NONE
+    xd = to_nhwc(x).to(dev)
+    K.x3_overflow(reset=True)
+    yw, yd = pw(xd, act=act), pd(xd, act=act)
+    yw2 = pw(xd, act=act)
+    torch.cuda.synchronize()
+    assert not K.x3_overflow(reset=True)
+    assert torch.equal(yw, yw2)  # deterministic (fixed reduction order, no atomics on data)
+    ew = float((from_nhwc(yw.cpu(), cout).double() - ref).abs().max())
+    ed = float((from_nhwc(yd.cpu(), cout).double() - ref).abs().max())
+    scale = float(ref.abs().max())
+    print(f"{case}: wr7 {ew / scale:.3e}, direct {ed / scale:.3e} of output scale")
+    assert ew / scale <= max(1.25 * ed / scale, 2e-7), (ew / scale, ed / scale)
+    assert ew / scale <= 1e-6
+
+
+def test_wr7_static_schedule_and_reserve(dev, monkeypatch):
+    """The static block-stride schedule (FVC_X3_DYN=0) and a CU reserve give the same bits."""
+    g = torch.Generator().manual_seed(3)
+    x = torch.relu(torch.randn(2, 32, 60, 100, generator=g))
+    w = torch.randn(64, 32, 7, 7, generator=g) * 0.03
+    b = torch.randn(64, generator=g) * 0.1
+    pw, _ = _packs(dev, w, b)
+    xd = to_nhwc(x).to(dev)
+    y0 = pw(xd, act=K.ACT_RELU)
+    monkeypatch.setenv("FVC_X3_DYN", "0")
+    y1 = pw(xd, act=K.ACT_RELU)
+    monkeypatch.setenv("FVC_X3_DYN", "1")
+    monkeypatch.setenv("FVC_X3_RESERVE", "200")
+    y2 = pw(xd, act=K.ACT_RELU)
+    torch.cuda.synchronize()
+    assert torch.equal(y0, y1) and torch.equal(y0, y2)
+
+
+def test_wr7_overflow_flag(dev):
+    """An activation whose transformed value leaves the fp16 range raises the stream's overflow
+    flag (the product then recomputes the frame on the fp32 kernels)."""
+    g = torch.Generator().manual_seed(5)
+    x = torch.relu(torch.randn(1, 32, 20, 40, generator=g))
+    x[0, 3, 10, 17] = 3e6
+    w = torch.randn(16, 32, 7, 7, generator=g) * 0.03
+    b = torch.zeros(16)
+    pw, _ = _packs(dev, w, b)
+    K.x3_overflow(reset=True)
+    pw(to_nhwc(x).to(dev), act=K.ACT_RELU)
+    torch.cuda.synchronize()
+    assert K.x3_overflow(reset=True)
+
+
+def test_wr7_spynet_layers_seeded(dev, seeded_sd):
+    """The pretrained SpyNet level-4 layers (the ones the bench runs at 1088x1920) on a ReLU'd
+    random input: error of scale vs float64 no worse than the direct kernel's."""
+    for name in ("conv2", "conv3", "conv4"):
+        w = seeded_sd[f"opticFlow.moduleBasic.3.{name}.weight"]
+        b = seeded_sd[f"opticFlow.moduleBasic.3.{name}.bias"]
+        cout, cin = w.shape[:2]
+        g = torch.Generator().manual_seed(11)
+        x = torch.relu(torch.randn(1, cin, 68, 120, generator=g))
+        ref = torch.relu(F.conv2d(x.double(), w.double(), b.double(), 1, 3))
+        pw, pd = _packs(dev, w, b)
+        xd = to_nhwc(x).to(dev)
+        yw, yd = pw(xd, act=K.ACT_RELU), pd(xd, act=K.ACT_RELU)
+        torch.cuda.synchronize()
+        scale = float(ref.abs().max())
+        ew = float((from_nhwc(yw.cpu(), cout).double() - ref).abs().max()) / scale
+        ed = float((from_nhwc(yd.cpu(), cout).double() - ref).abs().max()) / scale
+        print(f"SpyNet L4 {name}: wr7 {ew:.3e}, direct {ed:.3e} of output scale")
+        assert ew <= max(1.25 * ed, 2e-7), (name, ew, ed)

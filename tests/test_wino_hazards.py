@@ -52,3 +52,28 @@ def test_checker_flags_real_hazards():
     assert any("source" in b for b in bad) and any("dst touched" in b for b in bad), bad
     ok = "\tv_mfma_f32_16x16x32_f16 v[0:3], a[0:3], v[4:7], 0\n\ts_nop 4\n\tv_add_f32_e32 v8, v0, v1\n"
     assert mod.check(ok) == []
+
+
+@pytest.mark.skipif(not (os.path.exists(HIPCC) or shutil.which("hipcc")), reason="hipcc not available")
+def test_wr7_asm_wait_states(tmp_path):
+    """The same audit over every conv_wr7_kernel instantiation (fvc_conv_wr7.hip: inline-asm MFMAs
+    with U in AGPRs, the transformed-row ring written by VALU a step before its MFMAs read it)."""
+    from fastvideocodec_amd import build as B
+    src = os.path.join(REPO, "fastvideocodec_amd", "csrc", "fvc_conv_wr7.hip")
+    out = tmp_path / "wr7.s"
+    flags = [f for f in B.FLAGS if f != "-fPIC"] + B.SRC_FLAGS.get("fvc_conv_wr7.hip", [])
+    subprocess.run([HIPCC] + flags + ["--cuda-device-only", "-S", src, "-o", str(out)], check=True,
+                   stderr=subprocess.DEVNULL)
+    s = out.read_text()
+    mod = _checker()
+    import re
+    names = re.findall(r"^(_Z\S*conv_wr7_kernel\S*):", s, re.M)
+    assert len(names) == 18, names  # nt 1 / 2 x three modes x three activations
+    for n in names:
+        start = s.index(n + ":")
+        body = s[start:s.index(".Lfunc_end", start)]
+        bad = mod.check(body)
+        assert not bad, (n, bad[:5])
+        # U stays in AGPRs: loaded once, never copied in or out by the compiler
+        assert "v_accvgpr_write" not in body and "v_accvgpr_read" not in body, n
+        assert "scratch_" not in body, n
