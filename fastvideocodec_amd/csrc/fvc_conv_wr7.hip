@@ -54,11 +54,12 @@ constexpr int kCi = 32;                         // input channels per launch
 constexpr int kQ = kCi / 4;                     // channel quads
 constexpr int kSlots = 40;                      // column slots per (row, quad) line: 19 even + 19 odd used
 constexpr int kRowEntries = kQ * kSlots;        // 16-B entries per staged row (320 = 5 DMA pieces)
-constexpr int kRawRing = 8;                     // staged raw rows
-constexpr int kRawBytes = kRawRing * kRowEntries * 16;  // 40,960
+constexpr int kRawRing = 16;                    // staged raw rows
+constexpr int kRawBytes = kRawRing * kRowEntries * 16;  // 81,920
 constexpr int kZBytes = 4 * 2 * 2 * 64 * 16;            // partial outputs: [wave][i][n][lane] f32x4
 constexpr int kHdr = 256;                               // bias (128 B) + work-item word
-constexpr int kLds = kHdr + kRawBytes + 2 * kZBytes;    // 73,984
+constexpr int kResBytes = 4 * 3 * 64 * 16;             // residual rows (mode 2): [wave][3 slots][lane] f32x4
+constexpr int kLds = kHdr + kRawBytes + 2 * kZBytes + 1024 + kResBytes;  // 128,256 (+ the dummy-DMA sink)
 constexpr int kRows = 128;                      // output rows per work item
 constexpr float kLoScale = 2048.f;
 constexpr unsigned kOob = 0xFFFFFF00u;
@@ -129,6 +130,28 @@ __device__ __forceinline__ void split2(float v0, float v1, unsigned& hi, unsigne
       : "v"(r0), "v"(r1), "s"(kLoScale));
 }
 
+// One LDS-DMA piece (buffer_load_dwordx4 ... lds: 16 B per lane into LDS at M0 + 16 lane) in
+// inline asm. The builtin form makes hipcc wait for every pending LDS-DMA before each later
+// ds_read (it cannot tell the addresses apart), which would drain this kernel's row prefetch at
+// the first read of every step; in asm the DMA is invisible to hipcc's counters and the kernel
+// waits for it itself (the counted vmcnt + barrier at the end of each step). M0 is compiler-
+// reserved: set and restored inside the statement; s_nop 4 after the descriptor / M0 writes
+// (cdna_hip_programming.md §5.7 items 1-2).
+__device__ __forceinline__ void dma_piece(__amdgpu_buffer_rsrc_t rx, unsigned voff, const char* lds_dst) {
+  const unsigned base = __builtin_amdgcn_readfirstlane(
+      (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)lds_dst);
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %3\n\t"
+      "s_nop 4\n\t"
+      "buffer_load_dwordx4 %1, %2, 0 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(rx), "s"(base)
+      : "memory");
+}
+
 __device__ __forceinline__ float relu1(float x) {
   float r;
   asm("v_max_f32 %0, 0, %1" : "=v"(r) : "v"(x));
@@ -145,6 +168,8 @@ __global__ __launch_bounds__(256, 1) void conv_wr7_kernel(const Wr7Args a) {
   int* const sitem = reinterpret_cast<int*>(smem + 128);
   char* const raw = smem + kHdr;
   char* const zbuf = raw + kRawBytes;
+  char* const sink = zbuf + 2 * kZBytes;
+  char* const resb = sink + 1024;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -188,18 +213,19 @@ __global__ __launch_bounds__(256, 1) void conv_wr7_kernel(const Wr7Args a) {
     qa = 0.f; pb = 0.f; qb = 1.f; ya0 = 1.f; yb0 = 0.f; ya1 = 0.f; yb1 = 1.f;
   }
 
-  // DMA pieces of a staged row: piece k of 5 -> wave k & 3 (wave 0 also piece 4); the lane's entry
-  // (quad, column slot) -> input column and channel-quad offset. Column slots of a (row, quad) line:
-  // even strip columns 0..36 at 0..18, odd 1..37 at 19..37 (a tile's 8 columns are 2t + l)
+  // DMA pieces of a staged row: pieces 0..4 (320 entries); wave w issues piece w and, wave 0 only,
+  // piece 4 -- waves 1..3 issue a second, dummy piece into a sink so that every wave has the same
+  // number of vector-memory operations per step (the counted vmcnt below). The lane's entry
+  // (quad, column slot) -> input column and channel-quad offset. Column slots of a (row, quad)
+  // line: even strip columns 0..36 at 0..18, odd 1..37 at 19..37 (a tile's 8 columns are 2t + l)
   int dma_c[2], dma_q[2];
 #pragma unroll
   for (int m = 0; m < 2; ++m) {
     const int e = (wave + 4 * m) * 64 + lane;
     const int q = e / kSlots, cs = e - q * kSlots;
-    dma_c[m] = cs < 19 ? 2 * cs : (cs < 38 ? 2 * (cs - 19) + 1 : -(1 << 20));
+    dma_c[m] = (m == 1 && wave != 0) ? -(1 << 20) : (cs < 19 ? 2 * cs : (cs < 38 ? 2 * (cs - 19) + 1 : -(1 << 20)));
     dma_q[m] = 4 * q;
   }
-  const int npiece = wave == 0 ? 2 : 1;
   const unsigned row_bytes = (unsigned)W * a.xp * 4u;
   const unsigned rowe = (unsigned)W * a.xp;
   unsigned vo[2];
@@ -210,64 +236,70 @@ __global__ __launch_bounds__(256, 1) void conv_wr7_kernel(const Wr7Args a) {
       vo[m] = (unsigned)ix < (unsigned)W ? (unsigned)(ix * a.xp + dma_q[m]) * 4u : kOob;
     }
   };
-  // raw input row iy of image b into ring slot s (0 bytes for a padding row: the DMA lands zeros)
+  // raw input row iy of image b into raw ring slot `slot` (0 bytes for a padding row: the DMA
+  // lands zeros); two operations per wave
   auto stage_row = [&](const float* ximg, int iy, int slot) {
     const bool ok = (unsigned)iy < (unsigned)H;
     const __amdgpu_buffer_rsrc_t rx = rsrc(ximg + (size_t)(unsigned)(ok ? iy : 0) * rowe, ok ? row_bytes : 0u);
-#pragma unroll
-    for (int m = 0; m < 2; ++m) {
-      if (m >= npiece) break;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          rx, (lds_ptr)(raw + ((size_t)slot * kRowEntries + (wave + 4 * m) * 64) * 16), 16, vo[m], 0, 0, 0);
-    }
+    char* const rowp = raw + (size_t)slot * kRowEntries * 16;
+    dma_piece(rx, vo[0], rowp + (size_t)wave * 64 * 16);
+    dma_piece(rx, vo[1], wave == 0 ? rowp + 4 * 64 * 16 : sink);
   };
 
-  // the transformed-row ring (MFMA B operands, 2 positions x hi / lo): slot of input row r =
-  // (r - y0 + 3) & 7, the same as its raw slot
+  // the transformed-row ring (MFMA B operands, 2 positions x hi / lo): V slot of input row r =
+  // (r - y0 + 3) & 7 (compile-time in the 8-way unrolled row loop); raw slot (r - y0 + 3) & 15
   h8 vh[8][2], vl[8][2];
-  // transform raw slot RS into V slot RS: lane (t, o), channels 8o .. 8o + 7, positions a, b
-  auto transform = [&](auto RS_c) {
-    constexpr int RS = decltype(RS_c)::value;
-    const char* const row = raw + (size_t)RS * kRowEntries * 16;
+  // the transform of one input row in pieces, so that its VALU can sit between the MFMA blocks
+  // of a step: reads of one channel quad, the four channels of a quad, the splits
+  struct Tx {
+    float4 x[8];
     float va[8], vb[8];
-#pragma unroll
-    for (int hq = 0; hq < 2; ++hq) {
-      const char* const line = row + (size_t)(2 * o + hq) * kSlots * 16;
-      float4 x[8];
-#pragma unroll
-      for (int l = 0; l < 8; ++l) {
-        const int slot = (l & 1) ? 19 + t + (l >> 1) : t + (l >> 1);
-        x[l] = *reinterpret_cast<const float4*>(line + slot * 16);
-      }
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        auto ch = [&](const float4& v) { return c == 0 ? v.x : (c == 1 ? v.y : (c == 2 ? v.z : v.w)); };
-        const float e = fmaf(E3, ch(x[6]), fmaf(E2, ch(x[4]), fmaf(E1, ch(x[2]), E0 * ch(x[0]))));
-        const float od = fmaf(O3, ch(x[7]), fmaf(O2, ch(x[5]), fmaf(O1, ch(x[3]), O0 * ch(x[1]))));
-        va[4 * hq + c] = fmaf(qa, od, e);
-        vb[4 * hq + c] = fmaf(qb, od, pb * e);
-      }
-    }
     unsigned hwa[4], lwa[4], hwb[4], lwb[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      split2(va[2 * i], va[2 * i + 1], hwa[i], lwa[i]);
-      split2(vb[2 * i], vb[2 * i + 1], hwb[i], lwb[i]);
-    }
-    vh[RS][0] = __builtin_bit_cast(h8, v4u{hwa[0], hwa[1], hwa[2], hwa[3]});
-    vl[RS][0] = __builtin_bit_cast(h8, v4u{lwa[0], lwa[1], lwa[2], lwa[3]});
-    vh[RS][1] = __builtin_bit_cast(h8, v4u{hwb[0], hwb[1], hwb[2], hwb[3]});
-    vl[RS][1] = __builtin_bit_cast(h8, v4u{lwb[0], lwb[1], lwb[2], lwb[3]});
   };
-  // pin a transformed slot here in program order (its VALU writes may not sink towards the MFMAs
-  // that read it, which carry no wait states of their own past the first block of a kernel row)
-  auto pin = [&](auto RS_c) {
+  auto tx_read = [&](Tx& T, const char* row, int hq) {
+    const char* const line = row + (size_t)(2 * o + hq) * kSlots * 16;
+#pragma unroll
+    for (int l = 0; l < 8; ++l) {
+      const int slot = (l & 1) ? 19 + t + (l >> 1) : t + (l >> 1);
+      T.x[l] = *reinterpret_cast<const float4*>(line + slot * 16);
+    }
+  };
+  auto tx_chan = [&](Tx& T, int hq, int c) {
+    auto ch = [&](const float4& v) { return c == 0 ? v.x : (c == 1 ? v.y : (c == 2 ? v.z : v.w)); };
+    const float e = fmaf(E3, ch(T.x[6]), fmaf(E2, ch(T.x[4]), fmaf(E1, ch(T.x[2]), E0 * ch(T.x[0]))));
+    const float od = fmaf(O3, ch(T.x[7]), fmaf(O2, ch(T.x[5]), fmaf(O1, ch(T.x[3]), O0 * ch(T.x[1]))));
+    T.va[4 * hq + c] = fmaf(qa, od, e);
+    T.vb[4 * hq + c] = fmaf(qb, od, pb * e);
+  };
+  auto tx_split = [&](Tx& T, int i) {  // i < 4: V_a pair i, else V_b pair i - 4
+    if (i < 4) split2(T.va[2 * i], T.va[2 * i + 1], T.hwa[i], T.lwa[i]);
+    else split2(T.vb[2 * (i - 4)], T.vb[2 * (i - 4) + 1], T.hwb[i - 4], T.lwb[i - 4]);
+  };
+  auto tx_store = [&](Tx& T, auto RS_c) {
     constexpr int RS = decltype(RS_c)::value;
-    h8& h0 = vh[RS][0];  // (asm operands do not capture: name the ring slots through references)
+    vh[RS][0] = __builtin_bit_cast(h8, v4u{T.hwa[0], T.hwa[1], T.hwa[2], T.hwa[3]});
+    vl[RS][0] = __builtin_bit_cast(h8, v4u{T.lwa[0], T.lwa[1], T.lwa[2], T.lwa[3]});
+    vh[RS][1] = __builtin_bit_cast(h8, v4u{T.hwb[0], T.hwb[1], T.hwb[2], T.hwb[3]});
+    vl[RS][1] = __builtin_bit_cast(h8, v4u{T.lwb[0], T.lwb[1], T.lwb[2], T.lwb[3]});
+    // pin the slot here in program order: its VALU writes may not sink towards the MFMAs that read
+    // it (asm operands do not capture: name the ring slots through references)
+    h8& h0 = vh[RS][0];
     h8& l0 = vl[RS][0];
     h8& h1 = vh[RS][1];
     h8& l1 = vl[RS][1];
     asm volatile("" : "+v"(h0), "+v"(l0), "+v"(h1), "+v"(l1));
+  };
+  auto transform = [&](const char* row, auto RS_c) {  // whole row (prologue)
+    Tx T;
+#pragma unroll
+    for (int hq = 0; hq < 2; ++hq) {
+      tx_read(T, row, hq);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) tx_chan(T, hq, c);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) tx_split(T, i);
+    tx_store(T, RS_c);
   };
 
   // ---- schedule: items = (image, 32-column group, chunk of kRows output rows), chunk fastest
@@ -276,10 +308,51 @@ __global__ __launch_bounds__(256, 1) void conv_wr7_kernel(const Wr7Args a) {
   float chk = 0.f;
   const unsigned yrow_bytes = (unsigned)W * a.yp * 4u;
   // this lane's finishing share: output column parity fi and 16-channel tile fn (wave w -> (w & 1,
-  // w >> 1)); NT = 1 leaves waves 2 and 3 without one
+  // w >> 1)); NT = 1 leaves waves 2 and 3 without one (their stores / loads go to kOob)
   const int fi = wave & 1, fn = wave >> 1;
   const bool fin = fn < NT;
   int zb = 0;
+  // finishing of output row yf from the partial outputs in zbuf[zbf]: the four waves' partials
+  // summed in a fixed order, then scale, bias, the mode's partial sum, activation, 16-B store;
+  // live = false (no row before the item's first) issues the same memory operations to kOob
+  auto finish_row = [&](float* yimg, int yf, int zbf, unsigned so, bool live, const f32x4& rv) {
+    const __amdgpu_buffer_rsrc_t ry = rsrc(yimg + (size_t)(unsigned)yf * ((unsigned)W * a.yp), yrow_bytes);
+    const char* const zr = zbuf + zbf * kZBytes;
+    f32x4 sum = *reinterpret_cast<const f32x4*>(zr + (((0 * 2 + fi) * 2 + (fn & 1)) * 64 + lane) * 16);
+#pragma unroll
+    for (int w = 1; w < 4; ++w) sum += *reinterpret_cast<const f32x4*>(zr + (((w * 2 + fi) * 2 + (fn & 1)) * 64 + lane) * 16);
+    const f32x4 bj = *reinterpret_cast<const f32x4*>(sbias + 16 * (fn & 1) + 4 * o);
+    f32x4 v;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float tv = MODE == kModePartial ? sum[r] * a.osc : fmaf(sum[r], a.osc, bj[r]);
+      if constexpr (MODE == kModeAdd) tv += rv[r];
+      if constexpr (MODE != kModePartial) {
+        if constexpr (ACT == FVC_ACT_RELU) tv = relu1(tv);
+        if constexpr (ACT == FVC_ACT_LRELU) tv = fmaxf(tv, tv * 0.1f);
+      }
+      v[r] = tv;
+    }
+    if (live && fin) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) chk = fmaf(sum[r], 0.f, chk);
+    }
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v), ry, live ? so : kOob, 0, 0);
+  };
+  // the residual partial sum of output row yf (mode 2) into this wave's LDS slot yf % 3, by
+  // LDS-DMA like the raw rows (one operation per wave: the finishing lanes' 16 B each)
+  auto dma_res = [&](float* yimg, int yf, unsigned so_) {
+    if constexpr (MODE == kModeAdd) {
+      const bool ok = yf < H;
+      const __amdgpu_buffer_rsrc_t ry = rsrc(yimg + (size_t)(unsigned)(ok ? yf : 0) * ((unsigned)W * a.yp),
+                                             ok ? yrow_bytes : 0u);
+      dma_piece(ry, so_, resb + (size_t)(wave * 3 + (yf + 3) % 3) * 64 * 16);
+    }
+  };
+  auto res_of = [&](int yf) -> f32x4 {
+    if constexpr (MODE == kModeAdd) return *reinterpret_cast<const f32x4*>(resb + ((size_t)(wave * 3 + (yf + 3) % 3) * 64 + lane) * 16);
+    return f32x4{0.f, 0.f, 0.f, 0.f};
+  };
 
   for (;;) {
     if (tid == 0) sitem[0] = ctr ? atomicAdd(ctr, 1) : (int)blockIdx.x + k_item * (int)gridDim.x;
@@ -296,33 +369,55 @@ __global__ __launch_bounds__(256, 1) void conv_wr7_kernel(const Wr7Args a) {
     float* const yimg = a.y + (size_t)b * H * W * a.yp;
     row_offsets(g);
     // output byte offset of the finishing lane within an output row (past the row when the pixel
-    // is outside the image)
+    // is outside the image or the wave finishes nothing)
     const int ox = 32 * g + 2 * t + fi;
-    const unsigned so = ox < W ? (unsigned)(ox * a.yp + 16 * fn + 4 * o) * 4u : kOob;
+    const unsigned so = (ox < W && fin) ? (unsigned)(ox * a.yp + 16 * fn + 4 * o) * 4u : kOob;
+    auto raw_row = [&](int r) { return raw + (size_t)((r - y0 + 3) & (kRawRing - 1)) * kRowEntries * 16; };
 
-    // prologue: raw rows y0-3 .. y0+4 into slots 0..7, then the first 7 transformed rows
+    // prologue: raw rows y0-3 .. y0+5 (the first step's transform reads y0+4, the second's y0+5),
+    // then the first 7 transformed rows
 #pragma unroll
-    for (int i = 0; i < 8; ++i) stage_row(ximg, y0 - 3 + i, i);
+    for (int i = 0; i < 9; ++i) stage_row(ximg, y0 - 3 + i, i);
+    dma_res(yimg, y0, so);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    transform(ic<0>{}); transform(ic<1>{}); transform(ic<2>{}); transform(ic<3>{});
-    transform(ic<4>{}); transform(ic<5>{}); transform(ic<6>{});
-    pin(ic<0>{}); pin(ic<1>{}); pin(ic<2>{}); pin(ic<3>{}); pin(ic<4>{}); pin(ic<5>{}); pin(ic<6>{});
-    __syncthreads();  // every wave is done with raw slot 0 before step 0 stages into it
+    transform(raw_row(y0 - 3), ic<0>{}); transform(raw_row(y0 - 2), ic<1>{});
+    transform(raw_row(y0 - 1), ic<2>{}); transform(raw_row(y0), ic<3>{});
+    transform(raw_row(y0 + 1), ic<4>{}); transform(raw_row(y0 + 2), ic<5>{});
+    transform(raw_row(y0 + 3), ic<6>{});
+    __syncthreads();  // every wave is done with the prologue's raw slots before the steps stage
 
     int y = y0;
-    // one output row: S = (y - y0) & 7 (compile-time: the loop is unrolled by 8)
+    // one output row y, S = (y - y0) & 7 (compile-time: the loop is unrolled by 8). Program order:
+    // stage raw row y + 6; the previous row's residual; the 28 MFMA blocks of this row with, between
+    // them, the finishing of row y - 1 and the transform of raw row y + 4 into V slot (S + 7) & 7
+    // (a slot no kernel row of this step reads); drain; this row's partial outputs into zbuf[zb];
+    // counted vmcnt (raw row y + 5 landed) and the step's one barrier.
     auto step = [&](auto S_c) {
       constexpr int S = decltype(S_c)::value;
-      // raw row y + 5 into raw slot S (held row y - 3, transformed 7 steps ago)
-      stage_row(ximg, y + 5, S);
-      // the previous partial sum (second input-channel half): loaded now, used after the barrier
-      const __amdgpu_buffer_rsrc_t ry = rsrc(yimg + (size_t)(unsigned)y * ((unsigned)W * a.yp), yrow_bytes);
-      f32x4 rv = {0.f, 0.f, 0.f, 0.f};
-      if constexpr (MODE == kModeAdd)
-        if (fin) rv = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ry, so, 0, 0));
+      // the next row's partial sum (mode 2), finished two steps from now, then raw row y + 6
+      dma_res(yimg, y + 1, so);
+      stage_row(ximg, y + 6, (y + 9 - y0) & (kRawRing - 1));
+      const bool prev = y > y0;
+      const char* const rrow = raw_row(y + 4);
+      Tx T;
 
       f32x4 acc[2][NT], cor[2][NT];
+      int blk = 0;
+      // the VALU work placed after MFMA block k of the step (28 blocks)
+      auto gap = [&](int k) {
+        if (k == 0) tx_read(T, rrow, 0);
+        else if (k == 2) {
+          // the previous row's partial sum has landed once the 4 younger operations at most are
+          // pending: its store, this step's 2 DMA pieces and this row's load
+          finish_row(yimg, y - 1, zb ^ 1, so, prev, res_of(y - 1));
+        }
+        else if (k >= 3 && k <= 6) tx_chan(T, 0, k - 3);
+        else if (k == 7) tx_read(T, rrow, 1);
+        else if (k >= 8 && k <= 11) tx_chan(T, 1, k - 8);
+        else if (k >= 12 && k <= 19) tx_split(T, k - 12);
+        else if (k == 20) tx_store(T, ic<(S + 7) & 7>{});
+      };
       auto row_mfmas = [&](auto DY_c) {
         constexpr int DY = decltype(DY_c)::value;
         constexpr int VS = (S + DY) & 7;
@@ -330,25 +425,24 @@ __global__ __launch_bounds__(256, 1) void conv_wr7_kernel(const Wr7Args a) {
         for (int pp = 0; pp < 2; ++pp)
 #pragma unroll
           for (int n = 0; n < NT; ++n) {
-            if (pp == 0 && n == 0)
-              wr7_mfma3<DY == 0, true>(acc[pp][n], cor[pp][n], u[pp][DY][n][0], u[pp][DY][n][1], vh[VS][pp],
-                                       vl[VS][pp]);
+            if (DY == 0 && pp == 0 && n == 0)
+              wr7_mfma3<true, true>(acc[pp][n], cor[pp][n], u[pp][DY][n][0], u[pp][DY][n][1], vh[VS][pp], vl[VS][pp]);
             else
               wr7_mfma3<DY == 0, false>(acc[pp][n], cor[pp][n], u[pp][DY][n][0], u[pp][DY][n][1], vh[VS][pp],
                                         vl[VS][pp]);
+            gap(blk);
+            // NT = 1 has 14 blocks: two gaps' work per block
+            if constexpr (NT == 1) gap(blk + 1);
+            blk += NT == 1 ? 2 : 1;
           }
       };
       row_mfmas(ic<0>{});
       row_mfmas(ic<1>{});
       row_mfmas(ic<2>{});
-      // the next step's transformed row y + 4 (raw slot (S + 7) & 7, landed at the last barrier) into
-      // V slot (S + 7) & 7, which no kernel row of this step reads
-      transform(ic<(S + 7) & 7>{});
       row_mfmas(ic<3>{});
       row_mfmas(ic<4>{});
       row_mfmas(ic<5>{});
       row_mfmas(ic<6>{});
-      pin(ic<(S + 7) & 7>{});
       // 12 wait states after the last MFMA before any VALU reads an accumulator
       if constexpr (NT == 2)
         asm volatile("s_nop 11" : "+v"(acc[0][0]), "+v"(acc[0][NT - 1]), "+v"(acc[1][0]), "+v"(acc[1][NT - 1]),
@@ -371,39 +465,30 @@ __global__ __launch_bounds__(256, 1) void conv_wr7_kernel(const Wr7Args a) {
         *reinterpret_cast<f32x4*>(zw + (((wave * 2 + 0) * 2 + n) * 64 + lane) * 16) = p0;
         *reinterpret_cast<f32x4*>(zw + (((wave * 2 + 1) * 2 + n) * 64 + lane) * 16) = p1;
       }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA piece of raw row y + 5
+      // raw row y + 5 (staged one step ago) must have landed before the next step transforms it,
+      // and (mode 2) row y's partial sum, staged one step ago just before it: every wave issues per
+      // step [1 residual DMA,] 2 raw-row DMA operations and 1 store, so the ones younger than that
+      // row's DMA are the previous step's store and this step's 3 (4)
+      if constexpr (MODE == kModeAdd) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
       __syncthreads();
-      if (fin) {
-        f32x4 sum = *reinterpret_cast<const f32x4*>(zw + (((0 * 2 + fi) * 2 + fn) * 64 + lane) * 16);
-#pragma unroll
-        for (int w = 1; w < 4; ++w) sum += *reinterpret_cast<const f32x4*>(zw + (((w * 2 + fi) * 2 + fn) * 64 + lane) * 16);
-        const f32x4 bj = *reinterpret_cast<const f32x4*>(sbias + 16 * fn + 4 * o);
-        f32x4 v;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          chk = fmaf(sum[r], 0.f, chk);
-          float tv = MODE == kModePartial ? sum[r] * a.osc : fmaf(sum[r], a.osc, bj[r]);
-          if constexpr (MODE == kModeAdd) tv += rv[r];
-          if constexpr (MODE != kModePartial) {
-            if constexpr (ACT == FVC_ACT_RELU) tv = relu1(tv);
-            if constexpr (ACT == FVC_ACT_LRELU) tv = fmaxf(tv, tv * 0.1f);
-          }
-          v[r] = tv;
-        }
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v), ry, so, 0, 0);
-      }
       zb ^= 1;
       ++y;
     };
+    // the item's last row, after step S
+    auto last = [&](auto) {
+      finish_row(yimg, y1 - 1, zb ^ 1, so, true, res_of(y1 - 1));
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    };
     for (;;) {
-      step(ic<0>{}); if (y >= y1) break;
-      step(ic<1>{}); if (y >= y1) break;
-      step(ic<2>{}); if (y >= y1) break;
-      step(ic<3>{}); if (y >= y1) break;
-      step(ic<4>{}); if (y >= y1) break;
-      step(ic<5>{}); if (y >= y1) break;
-      step(ic<6>{}); if (y >= y1) break;
-      step(ic<7>{}); if (y >= y1) break;
+      step(ic<0>{}); if (y >= y1) { last(ic<0>{}); break; }
+      step(ic<1>{}); if (y >= y1) { last(ic<1>{}); break; }
+      step(ic<2>{}); if (y >= y1) { last(ic<2>{}); break; }
+      step(ic<3>{}); if (y >= y1) { last(ic<3>{}); break; }
+      step(ic<4>{}); if (y >= y1) { last(ic<4>{}); break; }
+      step(ic<5>{}); if (y >= y1) { last(ic<5>{}); break; }
+      step(ic<6>{}); if (y >= y1) { last(ic<6>{}); break; }
+      step(ic<7>{}); if (y >= y1) { last(ic<7>{}); break; }
     }
   }
   if (chk != 0.f && a.ovf) atomicOr(a.ovf, 1);

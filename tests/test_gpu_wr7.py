@@ -133,3 +133,21 @@ def test_wr7_spynet_layers_seeded(dev, seeded_sd):
         ed = float((from_nhwc(yd.cpu(), cout).double() - ref).abs().max()) / scale
         print(f"SpyNet L4 {name}: wr7 {ew:.3e}, direct {ed:.3e} of output scale")
         assert ew <= max(1.25 * ed, 2e-7), (name, ew, ed)
+
+
+@pytest.mark.parametrize("cin,cout", [(32, 64), (64, 32)])
+def test_wr7_many_items_per_block(dev, cin, cout):
+    """Several 128-row work items per block (4 x 600 x 640: 400 items on the persistent grid), the
+    path the small cases above leave out: every item boundary (raw-row ring, residual ring of the
+    partial-sum form, the deferred finishing of each item's last row) against the direct kernel,
+    and bit-identical on a second run (a ring slot read before its LDS-DMA landed would differ)."""
+    g = torch.Generator().manual_seed(1)
+    x = torch.relu(torch.randn(4, 600, 640, cin, generator=g)).to(dev)
+    w = torch.randn(cout, cin, 7, 7, generator=g) * (1.0 / (cin * 49) ** 0.5)
+    b = torch.randn(cout, generator=g) * 0.1
+    pw, pd = _packs(dev, w, b)
+    y1, y2, yd = pw(x, act=K.ACT_RELU), pw(x, act=K.ACT_RELU), pd(x, act=K.ACT_RELU)
+    torch.cuda.synchronize()
+    assert torch.equal(y1, y2)
+    err = float((y1 - yd).abs().max() / yd.abs().max())
+    assert err <= 4e-6, err
