@@ -195,22 +195,19 @@ __global__ __launch_bounds__(256, 1) void conv_wr7_kernel(const Wr7Args a) {
   if (tid < 16 * NT) sbias[tid] = (MODE != kModePartial && a.bias) ? a.bias[tid] : 0.f;
 
   // the wave's position pair (a, b) = (1,2), (3,4), (5,6), (0,7): e / o = the even / odd input
-  // columns' weighted sums (B^T rows, with the 2^-4 V scale), V_a = e + qa o, V_b = pb e + qb o;
-  // its share of the output transform: Y_i += ya_i M_a + yb_i M_b (A^T columns a, b)
+  // columns' weighted sums (B^T rows, with the 2^-4 V scale).
   const float s = 1.f / 16.f;
-  float E0, E1, E2, E3, O0, O1, O2, O3, qa, pb, qb, ya0, yb0, ya1, yb1;
+  // The partials a wave writes are P0 = M_a + M_b, P1 = M_a - M_b (waves 0..2) or P0 = M0, P1 = M7
+  // (wave 3); the A^T weights of P1 (1, 2, 1/2, 1 for waves 0..3) are applied by the finishing sum.
+  float E0, E1, E2, E3, O0, O1, O2, O3;
   if (wave == 0) {
     E0 = 0.f; E1 = s; E2 = -4.25f * s; E3 = s; O0 = s; O1 = -4.25f * s; O2 = s; O3 = 0.f;
-    qa = 1.f; pb = 1.f; qb = -1.f; ya0 = 1.f; yb0 = 1.f; ya1 = 1.f; yb1 = -1.f;
   } else if (wave == 1) {
     E0 = 0.f; E1 = 0.25f * s; E2 = -1.25f * s; E3 = s; O0 = 0.5f * s; O1 = -2.5f * s; O2 = 2.f * s; O3 = 0.f;
-    qa = 1.f; pb = 1.f; qb = -1.f; ya0 = 1.f; yb0 = 1.f; ya1 = 2.f; yb1 = -2.f;
   } else if (wave == 2) {
     E0 = 0.f; E1 = 4.f * s; E2 = -5.f * s; E3 = s; O0 = 2.f * s; O1 = -2.5f * s; O2 = 0.5f * s; O3 = 0.f;
-    qa = 1.f; pb = 1.f; qb = -1.f; ya0 = 1.f; yb0 = 1.f; ya1 = 0.5f; yb1 = -0.5f;
   } else {
     E0 = -s; E1 = 5.25f * s; E2 = -5.25f * s; E3 = s; O0 = -s; O1 = 5.25f * s; O2 = -5.25f * s; O3 = s;
-    qa = 0.f; pb = 0.f; qb = 1.f; ya0 = 1.f; yb0 = 0.f; ya1 = 0.f; yb1 = 1.f;
   }
 
   // DMA pieces of a staged row: pieces 0..4 (320 entries); wave w issues piece w and, wave 0 only,
@@ -252,7 +249,7 @@ __global__ __launch_bounds__(256, 1) void conv_wr7_kernel(const Wr7Args a) {
   // the transform of one input row in pieces, so that its VALU can sit between the MFMA blocks
   // of a step: reads of one channel quad, the four channels of a quad, the splits
   struct Tx {
-    float4 x[8];
+    float4 x0[8], x1[8];  // the lane's 8 columns of channel quads 2o and 2o + 1 (never live together)
     float va[8], vb[8];
     unsigned hwa[4], lwa[4], hwb[4], lwb[4];
   };
@@ -261,15 +258,26 @@ __global__ __launch_bounds__(256, 1) void conv_wr7_kernel(const Wr7Args a) {
 #pragma unroll
     for (int l = 0; l < 8; ++l) {
       const int slot = (l & 1) ? 19 + t + (l >> 1) : t + (l >> 1);
-      T.x[l] = *reinterpret_cast<const float4*>(line + slot * 16);
+      (hq ? T.x1 : T.x0)[l] = *reinterpret_cast<const float4*>(line + slot * 16);
     }
   };
+  // waves 0..2: V_a, V_b = e +- o over 3 + 3 columns (E0 = O3 = 0); wave 3: V0 = e, V7 = o over
+  // 4 + 4 columns (a wave-uniform branch: 8 VALU per channel either way)
   auto tx_chan = [&](Tx& T, int hq, int c) {
+    const float4* const x = hq ? T.x1 : T.x0;
     auto ch = [&](const float4& v) { return c == 0 ? v.x : (c == 1 ? v.y : (c == 2 ? v.z : v.w)); };
-    const float e = fmaf(E3, ch(T.x[6]), fmaf(E2, ch(T.x[4]), fmaf(E1, ch(T.x[2]), E0 * ch(T.x[0]))));
-    const float od = fmaf(O3, ch(T.x[7]), fmaf(O2, ch(T.x[5]), fmaf(O1, ch(T.x[3]), O0 * ch(T.x[1]))));
-    T.va[4 * hq + c] = fmaf(qa, od, e);
-    T.vb[4 * hq + c] = fmaf(qb, od, pb * e);
+    // (the empty asm keeps hipcc from if-converting the uniform branch into both paths + selects)
+    if (wave != 3) {
+      asm volatile("");
+      const float e = fmaf(E3, ch(x[6]), fmaf(E2, ch(x[4]), E1 * ch(x[2])));
+      const float od = fmaf(O2, ch(x[5]), fmaf(O1, ch(x[3]), O0 * ch(x[1])));
+      T.va[4 * hq + c] = e + od;
+      T.vb[4 * hq + c] = e - od;
+    } else {
+      asm volatile("");
+      T.va[4 * hq + c] = fmaf(E3, ch(x[6]), fmaf(E2, ch(x[4]), fmaf(E1, ch(x[2]), E0 * ch(x[0]))));
+      T.vb[4 * hq + c] = fmaf(O3, ch(x[7]), fmaf(O2, ch(x[5]), fmaf(O1, ch(x[3]), O0 * ch(x[1]))));
+    }
   };
   auto tx_split = [&](Tx& T, int i) {  // i < 4: V_a pair i, else V_b pair i - 4
     if (i < 4) split2(T.va[2 * i], T.va[2 * i + 1], T.hwa[i], T.lwa[i]);
@@ -315,30 +323,6 @@ __global__ __launch_bounds__(256, 1) void conv_wr7_kernel(const Wr7Args a) {
   // finishing of output row yf from the partial outputs in zbuf[zbf]: the four waves' partials
   // summed in a fixed order, then scale, bias, the mode's partial sum, activation, 16-B store;
   // live = false (no row before the item's first) issues the same memory operations to kOob
-  auto finish_row = [&](float* yimg, int yf, int zbf, unsigned so, bool live, const f32x4& rv) {
-    const __amdgpu_buffer_rsrc_t ry = rsrc(yimg + (size_t)(unsigned)yf * ((unsigned)W * a.yp), yrow_bytes);
-    const char* const zr = zbuf + zbf * kZBytes;
-    f32x4 sum = *reinterpret_cast<const f32x4*>(zr + (((0 * 2 + fi) * 2 + (fn & 1)) * 64 + lane) * 16);
-#pragma unroll
-    for (int w = 1; w < 4; ++w) sum += *reinterpret_cast<const f32x4*>(zr + (((w * 2 + fi) * 2 + (fn & 1)) * 64 + lane) * 16);
-    const f32x4 bj = *reinterpret_cast<const f32x4*>(sbias + 16 * (fn & 1) + 4 * o);
-    f32x4 v;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      float tv = MODE == kModePartial ? sum[r] * a.osc : fmaf(sum[r], a.osc, bj[r]);
-      if constexpr (MODE == kModeAdd) tv += rv[r];
-      if constexpr (MODE != kModePartial) {
-        if constexpr (ACT == FVC_ACT_RELU) tv = relu1(tv);
-        if constexpr (ACT == FVC_ACT_LRELU) tv = fmaxf(tv, tv * 0.1f);
-      }
-      v[r] = tv;
-    }
-    if (live && fin) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) chk = fmaf(sum[r], 0.f, chk);
-    }
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v), ry, live ? so : kOob, 0, 0);
-  };
   // the residual partial sum of output row yf (mode 2) into this wave's LDS slot yf % 3, by
   // LDS-DMA like the raw rows (one operation per wave: the finishing lanes' 16 B each)
   auto dma_res = [&](float* yimg, int yf, unsigned so_) {
@@ -354,6 +338,35 @@ __global__ __launch_bounds__(256, 1) void conv_wr7_kernel(const Wr7Args a) {
     return f32x4{0.f, 0.f, 0.f, 0.f};
   };
 
+  auto finish_read = [&](int zbf, int yf, f32x4 (&P)[4], f32x4& bj, f32x4& rv) {
+    const char* const zr = zbuf + zbf * kZBytes;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) P[w] = *reinterpret_cast<const f32x4*>(zr + (((w * 2 + fi) * 2 + (fn & 1)) * 64 + lane) * 16);
+    bj = *reinterpret_cast<const f32x4*>(sbias + 16 * (fn & 1) + 4 * o);
+    rv = res_of(yf);
+  };
+  // Y_fi = sum over waves of c_w P_w in a fixed order (c = 1 for Y0; 1, 2, 1/2, 1 for Y1), then
+  // scale, bias, the mode's partial sum, activation, 16-B store; live = false (no row before the
+  // item's first) issues the same memory operation to kOob
+  const float c1 = fi ? 2.f : 1.f, c2 = fi ? 0.5f : 1.f;
+  auto finish_row = [&](float* yimg, int yf, unsigned so, bool live, const f32x4 (&P)[4], const f32x4& bj,
+                        const f32x4& rv) {
+    const __amdgpu_buffer_rsrc_t ry = rsrc(yimg + (size_t)(unsigned)yf * ((unsigned)W * a.yp), yrow_bytes);
+    f32x4 v;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float sum = fmaf(c2, P[2][r], fmaf(c1, P[1][r], P[0][r])) + P[3][r];
+      if (live && fin) chk = fmaf(sum, 0.f, chk);
+      float tv = MODE == kModePartial ? sum * a.osc : fmaf(sum, a.osc, bj[r]);
+      if constexpr (MODE == kModeAdd) tv += rv[r];
+      if constexpr (MODE != kModePartial) {
+        if constexpr (ACT == FVC_ACT_RELU) tv = relu1(tv);
+        if constexpr (ACT == FVC_ACT_LRELU) tv = fmaxf(tv, tv * 0.1f);
+      }
+      v[r] = tv;
+    }
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v), ry, live ? so : kOob, 0, 0);
+  };
   for (;;) {
     if (tid == 0) sitem[0] = ctr ? atomicAdd(ctr, 1) : (int)blockIdx.x + k_item * (int)gridDim.x;
     ++k_item;
@@ -405,16 +418,19 @@ __global__ __launch_bounds__(256, 1) void conv_wr7_kernel(const Wr7Args a) {
       f32x4 acc[2][NT], cor[2][NT];
       int blk = 0;
       // the VALU work placed after MFMA block k of the step (28 blocks)
+      f32x4 P[4], bj, rv;
       auto gap = [&](int k) {
-        if (k == 0) tx_read(T, rrow, 0);
-        else if (k == 2) {
-          // the previous row's partial sum has landed once the 4 younger operations at most are
-          // pending: its store, this step's 2 DMA pieces and this row's load
-          finish_row(yimg, y - 1, zb ^ 1, so, prev, res_of(y - 1));
-        }
-        else if (k >= 3 && k <= 6) tx_chan(T, 0, k - 3);
-        else if (k == 7) tx_read(T, rrow, 1);
-        else if (k >= 8 && k <= 11) tx_chan(T, 1, k - 8);
+        // LDS reads two blocks ahead of their first use; quad 1's columns are read once quad 0's
+        // are consumed (the two sets never live together: VGPR budget)
+        if (k == 0) {
+          tx_read(T, rrow, 0);
+          finish_read(zb ^ 1, y - 1, P, bj, rv);
+        } else if (k == 2) tx_chan(T, 0, 0);
+        else if (k == 3) finish_row(yimg, y - 1, so, prev, P, bj, rv);
+        else if (k >= 4 && k <= 6) {
+          tx_chan(T, 0, k - 3);
+          if (k == 6) tx_read(T, rrow, 1);
+        } else if (k >= 8 && k <= 11) tx_chan(T, 1, k - 8);
         else if (k >= 12 && k <= 19) tx_split(T, k - 12);
         else if (k == 20) tx_store(T, ic<(S + 7) & 7>{});
       };
@@ -454,13 +470,17 @@ __global__ __launch_bounds__(256, 1) void conv_wr7_kernel(const Wr7Args a) {
       char* const zw = zbuf + zb * kZBytes;
 #pragma unroll
       for (int n = 0; n < NT; ++n) {
-        f32x4 p0, p1;
+        f32x4 ma, mb;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float ma = fmaf(cor[0][n][r], 1.f / kLoScale, acc[0][n][r]);
-          const float mb = fmaf(cor[1][n][r], 1.f / kLoScale, acc[1][n][r]);
-          p0[r] = fmaf(yb0, mb, ya0 * ma);
-          p1[r] = fmaf(yb1, mb, ya1 * ma);
+          ma[r] = fmaf(cor[0][n][r], 1.f / kLoScale, acc[0][n][r]);
+          mb[r] = fmaf(cor[1][n][r], 1.f / kLoScale, acc[1][n][r]);
+        }
+        f32x4 p0 = ma, p1 = mb;
+        if (wave != 3) {
+          asm volatile("");
+          p0 = ma + mb;
+          p1 = ma - mb;
         }
         *reinterpret_cast<f32x4*>(zw + (((wave * 2 + 0) * 2 + n) * 64 + lane) * 16) = p0;
         *reinterpret_cast<f32x4*>(zw + (((wave * 2 + 1) * 2 + n) * 64 + lane) * 16) = p1;
@@ -477,7 +497,9 @@ __global__ __launch_bounds__(256, 1) void conv_wr7_kernel(const Wr7Args a) {
     };
     // the item's last row, after step S
     auto last = [&](auto) {
-      finish_row(yimg, y1 - 1, zb ^ 1, so, true, res_of(y1 - 1));
+      f32x4 P[4], bj, rv;
+      finish_read(zb ^ 1, y1 - 1, P, bj, rv);
+      finish_row(yimg, y1 - 1, so, true, P, bj, rv);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     };
     for (;;) {
