@@ -46,6 +46,28 @@
 
 namespace {
 
+// experiment knobs (compile-time; the product build uses the defaults): the gap after which quad
+// 1's raw columns are read, and whether waves 0..2 use the 3 + 3-term transform (branch) or every
+// wave the general 4 + 4-term one (branch-free)
+#ifndef FVC_WR7_Q1GAP
+#define FVC_WR7_Q1GAP 4
+#endif
+#ifndef FVC_WR7_SPEC
+#define FVC_WR7_SPEC 0
+#endif
+#ifndef FVC_WR7_DIST
+#define FVC_WR7_DIST 2
+#endif
+// knock-outs (experiment builds only; results wrong): bit 0 no transform (raw reads + VALU),
+// bit 1 no finishing (partial reads, stores), bit 2 no per-step barrier, bit 3 no MFMAs, bit 4 no
+// partial-output writes (combine + ds_write)
+#ifndef FVC_WR7_KO
+#define FVC_WR7_KO 0
+#endif
+#ifndef FVC_WR7_SPREAD
+#define FVC_WR7_SPREAD 0
+#endif
+
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned v4u __attribute__((ext_vector_type(4)));
@@ -61,6 +83,7 @@ constexpr int kHdr = 256;                               // bias (128 B) + work-i
 constexpr int kResBytes = 4 * 3 * 64 * 16;             // residual rows (mode 2): [wave][3 slots][lane] f32x4
 constexpr int kLds = kHdr + kRawBytes + 2 * kZBytes + 1024 + kResBytes;  // 128,256 (+ the dummy-DMA sink)
 constexpr int kRows = 128;                      // output rows per work item
+constexpr int kDist = FVC_WR7_DIST;             // raw rows are staged kDist steps before their transform
 constexpr float kLoScale = 2048.f;
 constexpr unsigned kOob = 0xFFFFFF00u;
 constexpr int kRsrcFlags = 0x00020000;
@@ -267,7 +290,13 @@ __global__ __launch_bounds__(256, 1) void conv_wr7_kernel(const Wr7Args a) {
     const float4* const x = hq ? T.x1 : T.x0;
     auto ch = [&](const float4& v) { return c == 0 ? v.x : (c == 1 ? v.y : (c == 2 ? v.z : v.w)); };
     // (the empty asm keeps hipcc from if-converting the uniform branch into both paths + selects)
-    if (wave != 3) {
+    if (!FVC_WR7_SPEC) {
+      const float e = fmaf(E3, ch(x[6]), fmaf(E2, ch(x[4]), fmaf(E1, ch(x[2]), E0 * ch(x[0]))));
+      const float od = fmaf(O3, ch(x[7]), fmaf(O2, ch(x[5]), fmaf(O1, ch(x[3]), O0 * ch(x[1]))));
+      const bool w3 = wave == 3;
+      T.va[4 * hq + c] = w3 ? e : e + od;
+      T.vb[4 * hq + c] = w3 ? od : e - od;
+    } else if (wave != 3) {
       asm volatile("");
       const float e = fmaf(E3, ch(x[6]), fmaf(E2, ch(x[4]), E1 * ch(x[2])));
       const float od = fmaf(O2, ch(x[5]), fmaf(O1, ch(x[3]), O0 * ch(x[1])));
@@ -390,7 +419,7 @@ __global__ __launch_bounds__(256, 1) void conv_wr7_kernel(const Wr7Args a) {
     // prologue: raw rows y0-3 .. y0+5 (the first step's transform reads y0+4, the second's y0+5),
     // then the first 7 transformed rows
 #pragma unroll
-    for (int i = 0; i < 9; ++i) stage_row(ximg, y0 - 3 + i, i);
+    for (int i = 0; i < 7 + kDist; ++i) stage_row(ximg, y0 - 3 + i, i);
     dma_res(yimg, y0, so);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -410,7 +439,7 @@ __global__ __launch_bounds__(256, 1) void conv_wr7_kernel(const Wr7Args a) {
       constexpr int S = decltype(S_c)::value;
       // the next row's partial sum (mode 2), finished two steps from now, then raw row y + 6
       dma_res(yimg, y + 1, so);
-      stage_row(ximg, y + 6, (y + 9 - y0) & (kRawRing - 1));
+      stage_row(ximg, y + 4 + kDist, (y + 7 + kDist - y0) & (kRawRing - 1));
       const bool prev = y > y0;
       const char* const rrow = raw_row(y + 4);
       Tx T;
@@ -422,17 +451,21 @@ __global__ __launch_bounds__(256, 1) void conv_wr7_kernel(const Wr7Args a) {
       auto gap = [&](int k) {
         // LDS reads two blocks ahead of their first use; quad 1's columns are read once quad 0's
         // are consumed (the two sets never live together: VGPR budget)
+        if ((FVC_WR7_KO & 1) && k != 3 && k != 0) return;
+        if ((FVC_WR7_KO & 2) && k == 3) return;
         if (k == 0) {
-          tx_read(T, rrow, 0);
-          finish_read(zb ^ 1, y - 1, P, bj, rv);
+          if (!(FVC_WR7_KO & 1)) tx_read(T, rrow, 0);
+          if (!(FVC_WR7_KO & 2)) finish_read(zb ^ 1, y - 1, P, bj, rv);
         } else if (k == 2) tx_chan(T, 0, 0);
         else if (k == 3) finish_row(yimg, y - 1, so, prev, P, bj, rv);
-        else if (k >= 4 && k <= 6) {
-          tx_chan(T, 0, k - 3);
-          if (k == 6) tx_read(T, rrow, 1);
-        } else if (k >= 8 && k <= 11) tx_chan(T, 1, k - 8);
-        else if (k >= 12 && k <= 19) tx_split(T, k - 12);
-        else if (k == 20) tx_store(T, ic<(S + 7) & 7>{});
+        else if (k >= 4 && k <= 6) tx_chan(T, 0, k - 3);
+        else if (!FVC_WR7_SPREAD && k >= 8 && k <= 11) tx_chan(T, 1, k - 8);
+        else if (FVC_WR7_SPREAD && k >= 8 && k <= 14 && !(k & 1)) tx_chan(T, 1, (k - 8) >> 1);
+        else if (!FVC_WR7_SPREAD && k >= 12 && k <= 19) tx_split(T, k - 12);
+        else if (FVC_WR7_SPREAD && k >= 15 && k <= 26 && k != 17 && k != 20 && k != 23 && k != 26)
+          tx_split(T, k - 15 - (k > 17) - (k > 20) - (k > 23));
+        else if (k == (FVC_WR7_SPREAD ? 27 : 20)) tx_store(T, ic<(S + 7) & 7>{});
+        if (k == FVC_WR7_Q1GAP) tx_read(T, rrow, 1);
       };
       auto row_mfmas = [&](auto DY_c) {
         constexpr int DY = decltype(DY_c)::value;
@@ -441,7 +474,10 @@ __global__ __launch_bounds__(256, 1) void conv_wr7_kernel(const Wr7Args a) {
         for (int pp = 0; pp < 2; ++pp)
 #pragma unroll
           for (int n = 0; n < NT; ++n) {
-            if (DY == 0 && pp == 0 && n == 0)
+            if (FVC_WR7_KO & 8) {
+              if (DY == 0) acc[pp][n] = cor[pp][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+              asm volatile("" : "+v"(acc[pp][n]), "+v"(cor[pp][n]) : "v"(vh[VS][pp]), "v"(vl[VS][pp]));
+            } else if (DY == 0 && pp == 0 && n == 0)
               wr7_mfma3<true, true>(acc[pp][n], cor[pp][n], u[pp][DY][n][0], u[pp][DY][n][1], vh[VS][pp], vl[VS][pp]);
             else
               wr7_mfma3<DY == 0, false>(acc[pp][n], cor[pp][n], u[pp][DY][n][0], u[pp][DY][n][1], vh[VS][pp],
@@ -470,6 +506,10 @@ __global__ __launch_bounds__(256, 1) void conv_wr7_kernel(const Wr7Args a) {
       char* const zw = zbuf + zb * kZBytes;
 #pragma unroll
       for (int n = 0; n < NT; ++n) {
+        if (FVC_WR7_KO & 16) {
+          asm volatile("" :: "v"(acc[0][n]), "v"(acc[1][n]), "v"(cor[0][n]), "v"(cor[1][n]));
+          continue;
+        }
         f32x4 ma, mb;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -489,9 +529,10 @@ __global__ __launch_bounds__(256, 1) void conv_wr7_kernel(const Wr7Args a) {
       // and (mode 2) row y's partial sum, staged one step ago just before it: every wave issues per
       // step [1 residual DMA,] 2 raw-row DMA operations and 1 store, so the ones younger than that
       // row's DMA are the previous step's store and this step's 3 (4)
-      if constexpr (MODE == kModeAdd) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+      if constexpr (kDist == 3) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+      else if constexpr (MODE == kModeAdd) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      __syncthreads();
+      if (!(FVC_WR7_KO & 4)) __syncthreads();
       zb ^= 1;
       ++y;
     };

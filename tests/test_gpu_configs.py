@@ -144,11 +144,10 @@ def test_4k_gop32_one_rank_share(dev):
     (models.py:372-376's sequential loop, encode + rANS + decode). Checks: decoder recon == encoder
     recon bit for bit over all 31 P-frames, no split-precision overflow anywhere in the chain (31
     chained reconstructions at 4K, flag clear after frame 31), and frame 1's latents / PSNR vs the
-    CPU oracle: dPSNR <= 1e-4 dB, and symbol flips anchored to the fp32-MFMA convs on the same frame
-    (the split precision adds no flips beyond what an fp32 implementation shows against the
-    oracle; the reference itself flips 1.56e-5 of the symbols between two CPU backends at 1080p,
-    SURVEY §7, and SpyNet's warp-and-refine amplifies ulp differences more on 4K's larger flows:
-    measured r4 154 flips of 7.44 M = 2.1e-5 on the split path)."""
+    CPU oracle: dPSNR <= 1e-4 dB, and symbol flips no more than the reference's own flips on this
+    frame between its CPU backends / its fp32 and float64 runs (committed fixture, measured r5:
+    native 48, channels-last 30, 1 thread 2, float64 193 of 7.44 M) or the fp32-MFMA path's
+    (measured r4: split path 154, fp32 159)."""
     import os
 
     import bench
@@ -193,8 +192,20 @@ def test_4k_gop32_one_rank_share(dev):
     out, t = job.model(job.frames[:, 1].contiguous(), job.frames[:, 0].contiguous(), return_intermediates=True)
     torch.cuda.synchronize()
     nflip, ntot, per = flips(t)
-    print(f"4K frame 1 vs oracle: x3 {nflip} flips {per}, f32 {n32} flips {per32} of {ntot} symbols")
-    assert nflip <= max(1.5 * n32, n32 + 20), (nflip, n32, ntot)
+    # the bound is the reference's own flips on this frame, measured in the build
+    # container by tests/golden/gen_fullsize_parity.py (tests/golden/ref_fullsize_parity.json): the
+    # reference forward run under ATen's native convs, oneDNN on one thread, oneDNN channels-last
+    # and in float64, each against its default oneDNN run (which the oracle equals here: 0 flips).
+    # The largest, fp32 vs float64, is how far the reference's own fp32 arithmetic lands from the
+    # exact result; the fp32-MFMA path on the same frame is kept as the second anchor.
+    import json
+    with open(os.path.join(os.path.dirname(__file__), "golden", "ref_fullsize_parity.json")) as f:
+        k4 = json.load(f)["k4_frame1"]
+    assert k4["oracle_vs_onednn8"]["flips"]["total"] == 0 and ntot == k4["variants"]["native"]["n_symbols"]
+    ref_flips = {v: r["flips"]["total"] for v, r in k4["variants"].items()}
+    print(f"4K frame 1 vs oracle: x3 {nflip} flips {per}, f32 {n32} flips {per32} of {ntot} symbols; "
+          f"reference cross-backend {ref_flips}")
+    assert nflip <= max(max(ref_flips.values()), n32), (nflip, n32, ref_flips)
     sse_gpu = float(((out[0].cpu() - cur) ** 2).sum())
     sse_cpu = float(((o_clip - cur) ** 2).sum())
     dpsnr = abs(10 * np.log10(sse_cpu / sse_gpu))

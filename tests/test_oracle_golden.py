@@ -77,3 +77,20 @@ def test_warp_closed_form_edges():
     assert torch.allclose(w0[..., 0, 0], im[..., 0, 0]) and torch.allclose(w0[..., -1, -1], im[..., -1, -1])
     big = dvc_ref.warp(im, torch.full((2, 2, 5, 7), 1000.0))
     assert torch.allclose(big, im[..., -1:, -1:].expand_as(big))
+
+
+def test_fullsize_parity_fixture():
+    """tests/golden/ref_fullsize_parity.json (gen_fullsize_parity.py, run on the reference itself):
+    the oracle equals the reference at 1080p and 4K (0 flips), every backend variant covers every
+    symbol of the frame, and the GOP-12 chains have 11 P-frames each."""
+    import json
+    import os
+    with open(os.path.join(os.path.dirname(__file__), "golden", "ref_fullsize_parity.json")) as f:
+        d = json.load(f)
+    for key, n in (("p1080_frame1", 1860480), ("k4_frame1", 7441920)):
+        assert d[key]["oracle_vs_onednn8"]["flips"]["total"] == 0
+        for v in ("native", "onednn1", "chlast", "fp64"):
+            assert d[key]["variants"][v]["n_symbols"] == n
+    g = d["p1080_gop12"]
+    assert sorted(g["chains"]) == ["fp64", "native", "onednn8"]
+    assert all(len(c) == 11 for c in g["chains"].values())
