@@ -26,8 +26,9 @@ Outputs ``tests/golden/ref_fullsize_parity.json``:
 * ``p1080_frame1``: the same at 1920x1080 -> 1088 (GOP id 0, frame 1);
 * ``p1080_gop12``: BASELINE configs[2]'s closed loop -- one 1080p GOP-12 (GOP id 0) through the
   ``parallel_compression`` DVC-pretrained loop (``models.py:368-383``; frame 0 passed through as the
-  I-frame), per backend and per P-frame: PSNR (``models.py:379``), bpp and its three parts, symbol
-  statistics, and the flips / PSNR drift against the ``onednn8`` chain.
+  I-frame), per backend (``onednn8``, ``native``, ``fp64``, ``chlast``) and per P-frame: PSNR
+  (``models.py:379``), bpp and its three parts, symbol statistics, and the flips / PSNR drift
+  against the ``onednn8`` chain.
 
 The reference never leaves this container; only the JSON is committed.
 """
@@ -51,6 +52,7 @@ from fastvideocodec_amd.weights import seeded_torch_state_dict  # noqa: E402
 
 OUT = os.path.join(G.OUT, "ref_fullsize_parity.json")
 BAND_BYTES = 2 << 30
+GOP_VARIANTS = ("native", "fp64", "chlast")
 LATENTS = (("quant_mv", "mv"), ("compressed_feature", "feature"), ("compressed_z", "z"))
 
 _orig_conv_forward = torch.nn.Conv2d._conv_forward
@@ -283,6 +285,17 @@ def save(res):
 
 def main(which):
     res = load()
+    if which == "gop-add":
+        # add chains of the GOP_VARIANTS missing from an existing fixture (same anchor chain)
+        frames = make_gop(1080, 1920, 12, gop_seed(0))
+        g = res["p1080_gop12"]
+        _, anchor_runs = gop_chain(frames, "onednn8")
+        for v in GOP_VARIANTS:
+            if v not in g["chains"]:
+                g["chains"][v], _ = gop_chain(frames, v, anchor_runs)
+                g["psnr_drift_db"][v] = [c["vs_onednn8"]["dpsnr_db"] for c in g["chains"][v]]
+        save(res)
+        return
     if which in ("1080", "all"):
         frames = make_gop(1080, 1920, 12, gop_seed(0))
         r, runs = frame1(frames, ["onednn8", "native_unbanded", "native", "onednn1", "chlast", "fp64"], "p1080f1")
@@ -294,9 +307,9 @@ def main(which):
         chains = {}
         anchor_per, anchor_runs = gop_chain(frames, "onednn8")
         chains["onednn8"] = anchor_per
-        for v in ("native", "fp64"):
+        for v in GOP_VARIANTS:
             chains[v], _ = gop_chain(frames, v, anchor_runs)
-        drift = {v: [c["vs_onednn8"]["dpsnr_db"] for c in chains[v]] for v in ("native", "fp64")}
+        drift = {v: [c["vs_onednn8"]["dpsnr_db"] for c in chains[v]] for v in GOP_VARIANTS}
         res["p1080_gop12"] = {"frames": "make_gop(1080, 1920, 12, gop_seed(0)), closed loop models.py:368-383",
                               "chains": chains, "psnr_drift_db": drift}
         save(res)
@@ -310,4 +323,4 @@ def main(which):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1] if len(sys.argv) > 1 else "all")
+    main(sys.argv[1] if len(sys.argv) > 1 else "all")  # 4k | 1080 | all | gop-add
