@@ -772,7 +772,7 @@ def load_pmc_traffic(H, W, gops):
     over `bench.py --serial` (profiles/<round>/x3_traffic.json, written by scripts/rocprof_summary.py;
     FETCH_SIZE doubled per MI355X_MICROARCH.md's gfx950 correction). PMC passes serialise every
     dispatch and cannot run inside the timed region, so the figure is the profiled one."""
-    for rnd in ("r4", "r3", "r2", "r1"):
+    for rnd in ("r5", "r4", "r3", "r2", "r1"):
         path = os.path.join(REPO, "profiles", rnd, "x3_traffic.json")
         try:
             with open(path) as f:
