@@ -92,5 +92,5 @@ def test_fullsize_parity_fixture():
         for v in ("native", "onednn1", "chlast", "fp64"):
             assert d[key]["variants"][v]["n_symbols"] == n
     g = d["p1080_gop12"]
-    assert sorted(g["chains"]) == ["chlast", "fp64", "native", "onednn8"]
+    assert sorted(g["chains"]) == ["chlast", "fp64", "native", "onednn1", "onednn4", "onednn8"]
     assert all(len(c) == 11 for c in g["chains"].values())
