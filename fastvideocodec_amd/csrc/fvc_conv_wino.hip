@@ -49,19 +49,6 @@ namespace {
 #define FVC_STORE_AUX 0
 #endif
 
-// FVC_WINO_PIPE (r5): software-pipelined item loop -- the k-step-1 transform of an item runs in the
-// gaps of its k-step-0 MFMA blocks and the next item's k-step-0 transform in the gaps of its
-// k-step-1 blocks (rows staged two items ahead); 0 = the r4 loop (transforms up front)
-#ifndef FVC_WINO_PIPE
-#define FVC_WINO_PIPE 0
-#endif
-#ifndef FVC_WINO_SB
-#define FVC_WINO_SB 1
-#endif
-#ifndef FVC_WINO_DMA_BUILTIN
-#define FVC_WINO_DMA_BUILTIN 0
-#endif
-
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f2v __attribute__((ext_vector_type(2)));
@@ -72,16 +59,13 @@ constexpr int kC = 64;             // input and output channels
 constexpr int kQ = kC / 4;         // channel quads per pixel
 constexpr int kTiles = 16;         // tiles per item: one tile row x 16 tile columns
 constexpr int kCols = 2 * kTiles + 2;  // input columns an item reads
-constexpr int kSlots = 36;         // column slots per (row, quad) line (34 used; 9 whole DMA pieces a row)
-constexpr int kRowEntries = kQ * kSlots;   // 16-B entries per staged row (576)
+constexpr int kSlots = 40;         // column slots per (row, quad) line (34 used)
+constexpr int kRowEntries = kQ * kSlots;   // 16-B entries per staged row (640)
 constexpr int kRing = 8;           // staged input rows
-constexpr int kRingBytes = kRing * kRowEntries * 16;  // 73728
+constexpr int kRingBytes = kRing * kRowEntries * 16;  // 81920
 constexpr int kZBytes = 4 * 8 * 1024;                 // one Z buffer: 4 waves x 8 planes x 1 KB
 constexpr int kHdr = 512;                             // bias (256 B) + schedule words
-// pipelined loop: the item's residual (4 x 16 B per lane) arrives by LDS-DMA into a per-wave
-// region instead of 16 VGPRs held across the k-loop
-constexpr int kResBytes = FVC_WINO_PIPE ? 4 * 4 * 64 * 16 : 0;
-constexpr int kLds = kHdr + kRingBytes + 2 * kZBytes + kResBytes; // 156,160 B (pipelined)
+constexpr int kLds = kHdr + kRingBytes + 2 * kZBytes; // 148,480 B
 constexpr int kChunk = 16;         // items per schedule chunk (consecutive tile rows of one column)
 constexpr float kLoScale = 2048.f;
 // knock-outs (experiment builds only; results wrong): FVC_WINO_KO bit 1 = no k-step-1 MFMAs,
@@ -212,28 +196,6 @@ __device__ __forceinline__ void wino_mfma_drain(f32x4 (&acc)[4][4], f32x4 (&cor)
                "+v"(cor[3][1]), "+v"(cor[3][2]), "+v"(cor[3][3]));
 }
 
-// One LDS-DMA piece (buffer_load_dwordx4 ... lds, 16 B per lane into LDS at M0 + 16 lane) in inline
-// asm, for the pipelined loop: with the builtin form hipcc waits for every pending LDS-DMA before
-// each later ds_read (it cannot tell the addresses apart), which would drain the row prefetch at the
-// first transform read of every item; in asm the DMA is invisible to hipcc's counters and the kernel
-// waits for it itself (vmcnt(0) + the item barrier). M0 is compiler-reserved: saved and restored
-// inside the statement; s_nop 4 after the M0 write (cdna_hip_programming.md §5.7).
-// lds_addr: the destination's LDS byte address (formed from the kernel's LDS base: a generic -> LDS
-// cast of a derived pointer trips an instruction-selection bug in this hipcc)
-__device__ __forceinline__ void dma_piece(__amdgpu_buffer_rsrc_t rx, unsigned voff, unsigned lds_addr) {
-  const unsigned base = __builtin_amdgcn_readfirstlane(lds_addr);
-  unsigned keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\t"
-      "s_mov_b32 m0, %3\n\t"
-      "s_nop 4\n\t"
-      "buffer_load_dwordx4 %1, %2, 0 offen lds\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(voff), "s"(rx), "s"(base)
-      : "memory");
-}
-
 // max(x, 0) as one v_max_f32 (fmaxf compiles to a NaN-quieting v_max x, x first)
 __device__ __forceinline__ float relu1(float x) {
   float r;
@@ -267,9 +229,6 @@ __global__ __launch_bounds__(256, 1) void conv_wino_kernel(const WinoArgs a) {
   int* const sq = reinterpret_cast<int*>(smem + 256);  // [0..1] first chunks, [2..3] chunk after next
   char* const ring = smem + kHdr;
   char* const zbuf = ring + kRingBytes;
-  char* const resb = zbuf + 2 * kZBytes;  // pipelined loop: [wave][i][j][lane] residual
-  const unsigned smem_lds = (unsigned)(uintptr_t)(lds_ptr)smem;
-  auto lds_addr = [&](const char* p) { return smem_lds + (unsigned)(p - smem); };
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -310,7 +269,7 @@ __global__ __launch_bounds__(256, 1) void conv_wino_kernel(const WinoArgs a) {
     dma_lc[m] = cs < 17 ? 2 * cs : (cs < 34 ? 2 * (cs - 17) + 1 : -(1 << 20));
     dma_ch[m] = 4 * c4;
   }
-  const int npiece = (kRowEntries / 64 - wave + 3) / 4;  // 9 pieces over 4 waves
+  const int npiece = wave < 2 ? 3 : 2;  // 10 pieces over 4 waves
   // byte offsets of the lane's pieces within an input row of column group g (past the row for
   // padding columns and pad slots: the buffer unit returns zeros)
   auto row_offsets = [&](int g, unsigned (&vo)[3]) {
@@ -392,140 +351,6 @@ __global__ __launch_bounds__(256, 1) void conv_wino_kernel(const WinoArgs a) {
       po = px < Wp ? (unsigned)(px * kC + cbase) * 4u : kOob;
     }
   };
-  // ---- column combination Z[r][j] = sum_q M[r][q] A[q][j] of an item (M in units of 2^kw: the
-  // scale is applied once on Y) -> LDS plane (r, j, n) of Z buffer zw, lane-linear
-  auto combine = [&](char* const zw, const f32x4 (&acc)[4][4], const f32x4 (&cor)[4][4]) {
-#pragma unroll
-    for (int n = 0; n < 4; ++n) {
-      f32x4 z0, z1;
-      const f2v ls2 = {1.f / kLoScale, 1.f / kLoScale};
-#pragma unroll
-      for (int cp = 0; cp < 2; ++cp) {
-        f2v m[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const f2v c2 = cp ? f2v{cor[q][n][2], cor[q][n][3]} : f2v{cor[q][n][0], cor[q][n][1]};
-          const f2v a2 = cp ? f2v{acc[q][n][2], acc[q][n][3]} : f2v{acc[q][n][0], acc[q][n][1]};
-          m[q] = __builtin_elementwise_fma(c2, ls2, a2);
-        }
-        const f2v p0 = (m[0] + m[1]) + m[2], p1 = (m[1] - m[2]) - m[3];
-        z0[2 * cp] = p0.x; z0[2 * cp + 1] = p0.y;
-        z1[2 * cp] = p1.x; z1[2 * cp + 1] = p1.y;
-      }
-      *reinterpret_cast<f32x4*>(zw + ((wave * 2 + 0) * 4 + n) * 1024 + lane * 16) = z0;
-      *reinterpret_cast<f32x4*>(zw + ((wave * 2 + 1) * 4 + n) * 1024 + lane * 16) = z1;
-    }
-  };
-  // ---- finishing pass of item ty (tile row) from Z buffer zw: wave w -> output channels
-  // 16w..16w+15 of the item's 16 tiles; ry spans the item's output band, rv its residual
-  auto finishing = [&](char* const zw, const int ty, const __amdgpu_buffer_rsrc_t& ry, const f32x4 (&rv)[2][2]) {
-    if constexpr (!(FVC_WINO_KO & 8)) {
-    f32x4 z[4][2];
-#pragma unroll
-    for (int p = 0; p < 4; ++p)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-        if constexpr (FVC_WINO_KO & 32) {
-          z[p][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-          asm volatile("" : "+v"(z[p][j]));
-        } else {
-          z[p][j] = *reinterpret_cast<const f32x4*>(zw + ((p * 2 + j) * 4 + wave) * 1024 + lane * 16);
-        }
-    const f32x4 bj = *reinterpret_cast<const f32x4*>(sbias + cbase);
-    f32x4 yv[2][2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        f32x4 vv;
-#pragma unroll
-        for (int cp = 0; cp < 2; ++cp) {
-          auto pr = [&](const f32x4& x) { return cp ? f2v{x[2], x[3]} : f2v{x[0], x[1]}; };
-          const f2v ys = i == 0 ? (pr(z[0][j]) + pr(z[1][j])) + pr(z[2][j]) : (pr(z[1][j]) - pr(z[2][j])) - pr(z[3][j]);
-          chk2 = __builtin_elementwise_fma(ys, f2v{0.f, 0.f}, chk2);
-          f2v tv = __builtin_elementwise_fma(ys, f2v{a.osc, a.osc}, pr(bj));
-          if constexpr (RES == kResPre) tv += pr(rv[i][j]);
-          if constexpr (ACT == FVC_ACT_RELU) tv = f2v{relu1(tv.x), relu1(tv.y)};
-          if constexpr (ACT == FVC_ACT_LRELU) {
-            const f2v t1 = tv * f2v{0.1f, 0.1f};
-            tv = f2v{fmaxf(tv.x, t1.x), fmaxf(tv.y, t1.y)};
-          }
-          if constexpr (RES == kResPost) tv += pr(rv[i][j]);
-          vv[2 * cp] = tv.x;
-          vv[2 * cp + 1] = tv.y;
-        }
-        yv[i][j] = vv;
-        if constexpr (POST != kPostTap) {
-          if constexpr (FVC_WINO_KO & 16) asm volatile("" ::"v"(vv));
-          else __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, vv), ry, yo[i][j], 0, FVC_STORE_AUX);
-        }
-      }
-    if constexpr (POST == kPostPool) {
-      f32x4 pv;
-#pragma unroll
-      for (int c = 0; c < 4; ++c) pv[c] = (((yv[0][0][c] + yv[0][1][c]) + yv[1][0][c]) + yv[1][1][c]) / 4.f;
-      const __amdgpu_buffer_rsrc_t rp =
-          rsrc(a.pool + ((size_t)cur.b * Hp + ty) * Wp * kC, ty < Hp ? (unsigned)Wp * kC * 4u : 0u);
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, pv), rp, po, 0, 0);
-    }
-    if constexpr (POST == kPostTap) {
-      // y never reaches HBM: each wave parks its 16 channels of the item's 64 pixels in its own
-      // planes of this item's Z buffer (no other wave read them), then wave v multiplies the
-      // 64-channel y of pixel (i, j) = (v >> 1, v & 1) of the 16 tiles with the next layer's tap
-      // weights: P [16 partials x 16 tiles] per row tile on v_mfma_f32_16x16x32_f16, split
-      // precision (main = T_hi y_hi, corr = T_lo y_hi + T_hi y_lo), P = main 2^-kt + corr 2^-kt-11.
-      // Z(zb) is next written two items later, behind the next item's barrier.
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          *reinterpret_cast<f32x4*>(zw + ((i * 2 + j) * 4 + wave) * 1024 + lane * 16) = yv[i][j];
-#pragma unroll
-          for (int c = 0; c < 4; ++c) mxy = fmaxf(mxy, fabsf(yv[i][j][c]));
-        }
-      __syncthreads();
-      const int pi = wave >> 1, pj = wave & 1;
-      h8 th[2], tl[2];
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        // B operand: lane (t, q = lane >> 4) holds channels 32 kk + 8 q .. + 7 of tile t = quads
-        // 2 (q & 1), +1 of wave 2 kk + (q >> 1)
-        const char* src = zw + ((pi * 2 + pj) * 4 + 2 * kk + (lane >> 5)) * 1024 + ((2 * ((lane >> 4) & 1)) * 16 + t) * 16;
-        const f32x4 q0 = *reinterpret_cast<const f32x4*>(src);
-        const f32x4 q1 = *reinterpret_cast<const f32x4*>(src + 256);
-        unsigned hw[4], lw[4];
-        split2(q0[0], q0[1], hw[0], lw[0]);
-        split2(q0[2], q0[3], hw[1], lw[1]);
-        split2(q1[0], q1[1], hw[2], lw[2]);
-        split2(q1[2], q1[3], hw[3], lw[3]);
-        th[kk] = __builtin_bit_cast(h8, v4u{hw[0], hw[1], hw[2], hw[3]});
-        tl[kk] = __builtin_bit_cast(h8, v4u{lw[0], lw[1], lw[2], lw[3]});
-      }
-      const int ox = 32 * cur.g + 2 * t + pj;
-#pragma unroll
-      for (int rt = 0; rt < 2; ++rt) {
-        f32x4 pa = {0.f, 0.f, 0.f, 0.f}, pc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk) {
-          const uint4* const tw = a.tw + (size_t)((rt * 2 + kk) * 2) * 64 + lane;
-          const h8 wh = __builtin_bit_cast(h8, tw[0]);
-          const h8 wl = __builtin_bit_cast(h8, tw[64]);
-          pa = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, th[kk], pa, 0, 0, 0);
-          pc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl, th[kk], pc, 0, 0, 0);
-          pc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, tl[kk], pc, 0, 0, 0);
-        }
-        const int p0 = rt * 16 + 4 * (lane >> 4);
-        f32x4 o;
-#pragma unroll
-        for (int c = 0; c < 4; ++c) o[c] = fmaf(pc[c], a.tosc_c, pa[c] * a.tosc);
-        const unsigned so = (ox < W && p0 < a.pcp) ? (unsigned)((pi * W + ox) * a.pcp + p0) * 4u : kOob;
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, o), ry, so, 0, 0);
-      }
-    }
-
-    }  // FVC_WINO_KO & 8
-  };
-
   unsigned vo_cur[3];
   // image bases of the current chunk (x, the output y / tap partials P, the residual)
   const unsigned ype = POST == kPostTap ? (unsigned)a.pcp : (unsigned)a.yp;
@@ -534,220 +359,6 @@ __global__ __launch_bounds__(256, 1) void conv_wino_kernel(const WinoArgs a) {
   float* yi_cur = a.y + (size_t)cur.b * yimg_e;
   const float* ri_cur = RES ? a.res + (size_t)cur.b * H * W * a.yp : nullptr;
 
-#if FVC_WINO_PIPE
-  // ---- pipelined item loop. An item's V operands are built in two halves (k-steps) between MFMA
-  // blocks: its k-step-1 operands in the gaps of its own k-step-0 blocks, the NEXT item's k-step-0
-  // operands in the gaps of its k-step-1 blocks (reading the next item's rows, which therefore
-  // land one item earlier: rows are staged two items ahead). Chunk starts break the chain: the
-  // first two items of a chunk ("cold", position d = 0, 1 in the chunk) transform their k-step 0
-  // up front, items d >= 2 ("warm") arrive with it built. Ring use (8 slots) with item k's window
-  // at slots base .. base + 3: item k + 1 at base + 2 .. base + 5, the new rows of item k + 2 at
-  // base + 6, base + 7 (the slots of item k - 1's first rows, free after its barrier); the rows of
-  // a cold item are staged one item ahead exactly as in the r4 loop.
-  //
-  // one k-step's operands in pieces placed after MFMA blocks k = 0 .. 13: reads of channel half 0,
-  // its transform, its splits per position, then the same for half 1 (one half's raw or
-  // transformed values live at a time: VGPR budget)
-  struct Tx {
-    float4 da[4], db[4];
-    f2v v[4][2];              // position q, channel pair cp of the current half
-    unsigned hw[4][4], lw[4][4];  // position q, channel pair 2 hh + cp: split hi / lo words
-  };
-  auto tx_read = [&](Tx& T, const char* pa, const char* pb, int kk, int hh) {
-    // patch columns 0..3 of tile t: slots t, 17 + t, t + 1, 18 + t (even / odd column halves)
-    const int e0 = ((8 * kk + 2 * o + hh) * kSlots + t) * 16;
-    T.da[0] = *reinterpret_cast<const float4*>(pa + e0);
-    T.da[1] = *reinterpret_cast<const float4*>(pa + e0 + 17 * 16);
-    T.da[2] = *reinterpret_cast<const float4*>(pa + e0 + 16);
-    T.da[3] = *reinterpret_cast<const float4*>(pa + e0 + 18 * 16);
-    T.db[0] = *reinterpret_cast<const float4*>(pb + e0);
-    T.db[1] = *reinterpret_cast<const float4*>(pb + e0 + 17 * 16);
-    T.db[2] = *reinterpret_cast<const float4*>(pb + e0 + 16);
-    T.db[3] = *reinterpret_cast<const float4*>(pb + e0 + 18 * 16);
-  };
-  const f2v sb2 = {sb, sb};
-  // V[q] = E B for channel pair cp of the half in T (E = d[ra] + sb d[rb])
-  auto tx_tf = [&](Tx& T, int cp) {
-    f2v e[4];
-#pragma unroll
-    for (int jj = 0; jj < 4; ++jj) {
-      f2v xa = cp ? f2v{T.da[jj].z, T.da[jj].w} : f2v{T.da[jj].x, T.da[jj].y};
-      f2v xb = cp ? f2v{T.db[jj].z, T.db[jj].w} : f2v{T.db[jj].x, T.db[jj].y};
-      if constexpr (IOP == FVC_IN_RELU) {
-        xa = f2v{relu1(xa.x), relu1(xa.y)};
-        xb = f2v{relu1(xb.x), relu1(xb.y)};
-      }
-      e[jj] = __builtin_elementwise_fma(sb2, xb, xa);
-    }
-    T.v[0][cp] = e[0] - e[2];
-    T.v[1][cp] = e[1] + e[2];
-    T.v[2][cp] = e[2] - e[1];
-    T.v[3][cp] = e[1] - e[3];
-  };
-  auto tx_split = [&](Tx& T, int q, int hh) {
-#pragma unroll
-    for (int cp = 0; cp < 2; ++cp) split2(T.v[q][cp].x, T.v[q][cp].y, T.hw[q][2 * hh + cp], T.lw[q][2 * hh + cp]);
-  };
-  auto tx_piece = [&](Tx& T, int k, const char* pa, const char* pb, int kk) {
-    if (k == 0 || k == 7) tx_read(T, pa, pb, kk, k == 7);
-    else if (k == 2 || k == 9) {
-      tx_tf(T, 0);
-      tx_tf(T, 1);
-    } else if (k >= 3 && k <= 6) tx_split(T, k - 3, 0);
-    else if (k >= 10 && k <= 13) tx_split(T, k - 10, 1);
-  };
-  auto tx_out = [&](Tx& T, h8 (&vh)[4], h8 (&vl)[4]) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      vh[q] = __builtin_bit_cast(h8, v4u{T.hw[q][0], T.hw[q][1], T.hw[q][2], T.hw[q][3]});
-      vl[q] = __builtin_bit_cast(h8, v4u{T.lw[q][0], T.lw[q][1], T.lw[q][2], T.lw[q][3]});
-    }
-    // pin the operands here in program order (their VALU may not sink towards the MFMAs)
-    asm volatile("" : "+v"(vh[0]), "+v"(vh[1]), "+v"(vh[2]), "+v"(vh[3]));
-    asm volatile("" : "+v"(vl[0]), "+v"(vl[1]), "+v"(vl[2]), "+v"(vl[3]));
-  };
-  // LDS-DMA of input row iy into ring slot s (asm pieces: no compiler waits)
-  auto stage_row_a = [&](const float* ximg, int iy, int s, const unsigned (&vo)[3]) {
-    const bool row_ok = (unsigned)iy < (unsigned)H;
-    const __amdgpu_buffer_rsrc_t rx = rsrc(ximg + (size_t)(unsigned)(row_ok ? iy : 0) * rowe, row_ok ? row_bytes : 0u);
-#pragma unroll
-    for (int m = 0; m < 3; ++m) {
-      if (m >= npiece) break;
-#if FVC_WINO_DMA_BUILTIN  // debug builds only: the builtin form (hipcc then waits on it before ds_reads)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          rx, (lds_ptr)(ring + ((size_t)(s & (kRing - 1)) * kRowEntries + (wave + 4 * m) * 64) * 16), 16, vo[m], 0, 0, 0);
-#else
-      dma_piece(rx, vo[m], lds_addr(ring + ((size_t)(s & (kRing - 1)) * kRowEntries + (wave + 4 * m) * 64) * 16));
-#endif
-    }
-  };
-  auto slot = [&](int s) { return ring + (size_t)(s & (kRing - 1)) * kRowEntries * 16; };
-
-  if (cur.ty0 < cur.ty1) {
-    row_offsets(cur.g, vo_cur);
-    out_offsets(cur.g);
-    for (int i = 0; i < 4; ++i) stage_row_a(xi_cur, 2 * cur.ty0 - 1 + i, i, vo_cur);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    int ty = cur.ty0;
-    int base = 0;  // ring slot of the current item's first row
-    int zb = 0;    // Z buffer
-    h8 vh0[4], vl0[4];  // k-step-0 operands of the current item (built by the previous one when warm)
-    for (;;) {
-      const bool first = ty == cur.ty0;
-      const bool cont = ty + 1 < cur.ty1;  // the next item continues down this column
-      const int nty = cont ? ty + 1 : nxt.ty0;
-      const bool nvalid = cont || nxt.ty0 < nxt.ty1;
-      const int nbase = (base + (cont ? 2 : 4)) & (kRing - 1);
-      const bool warm = ty - cur.ty0 >= 2;
-      if (first && tid == 0) sq[2 + (ntaken & 1)] = take(ntaken);  // chunk after next
-
-      // row staging: a cold next item's rows (its 4-row window after a chunk change, or the 2 new
-      // rows of a chunk's second item), and the 2 new rows of the item after next in this chunk
-      if (nvalid && (first || !cont)) {
-        if (cont) {
-          for (int i = 2; i < 4; ++i) stage_row_a(xi_cur, 2 * nty - 1 + i, nbase + i, vo_cur);
-        } else {
-          unsigned vo[3];
-          row_offsets(nxt.g, vo);
-          const float* xi_np = a.x + (size_t)nxt.b * ximg_e;
-          for (int i = 0; i < 4; ++i) stage_row_a(xi_np, 2 * nty - 1 + i, nbase + i, vo);
-        }
-      }
-      if (ty + 2 < cur.ty1)
-        for (int i = 2; i < 4; ++i) stage_row_a(xi_cur, 2 * (ty + 2) - 1 + i, base + 4 + i, vo_cur);
-
-      // the finishing pass's output band and residual (loaded now: its latency hides behind the
-      // k-loop)
-      const unsigned band_rows = 2 * ty + 1 < H ? 2u : 1u;
-      const unsigned band_bytes = band_rows * yrow_bytes;
-      const __amdgpu_buffer_rsrc_t ry = rsrc(yi_cur + (size_t)(unsigned)(2 * ty) * ((unsigned)W * ype),
-                                             band_rows * (unsigned)W * ype * 4u);
-      if constexpr (RES) {
-        const __amdgpu_buffer_rsrc_t rr = rsrc(ri_cur + (size_t)(unsigned)(2 * ty) * ((unsigned)W * a.yp), band_bytes);
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-          for (int j = 0; j < 2; ++j) dma_piece(rr, yo[i][j], lds_addr(resb + (size_t)(wave * 4 + i * 2 + j) * 64 * 16));
-      }
-
-      const char* const rowa = slot(base + ra);
-      const char* const rowb = slot(base + rb);
-      if (!warm) {  // cold item: k-step-0 operands now
-        Tx T;
-#pragma unroll
-        for (int k = 0; k < 14; ++k) tx_piece(T, k, rowa, rowb, 0);
-        tx_out(T, vh0, vl0);
-      }
-
-      // ---- k-loop: 2 steps of 32 input channels, 16 blocks of 3 MFMAs each
-      f32x4 acc[4][4], cor[4][4];
-      h8 vh1[4], vl1[4];
-      {
-        Tx T;
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-#pragma unroll
-          for (int n = 0; n < 4; ++n) {
-            // k-step 0 starts every accumulator chain from C = 0
-            if (n == 0 || kAllNop) wino_mfma3<true, true>(acc[q][n], cor[q][n], u[q][n][0][0], u[q][n][0][1], vh0[q], vl0[q]);
-            else wino_mfma3<true, false>(acc[q][n], cor[q][n], u[q][n][0][0], u[q][n][0][1], vh0[q], vl0[q]);
-            tx_piece(T, 4 * q + n, rowa, rowb, 1);
-            if constexpr (FVC_WINO_SB) __builtin_amdgcn_sched_barrier(0);  // keep each gap's work between its MFMA blocks
-          }
-        tx_out(T, vh1, vl1);
-      }
-      {
-        // the next item's k-step 0 (used only when that item is warm: its rows are in the ring;
-        // otherwise the values are discarded and the item transforms cold)
-        const char* const nrowa = slot(nbase + ra);
-        const char* const nrowb = slot(nbase + rb);
-        Tx T;
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-#pragma unroll
-          for (int n = 0; n < 4; ++n) {
-            if (n == 0 || kAllNop) wino_mfma3<false, true>(acc[q][n], cor[q][n], u[q][n][1][0], u[q][n][1][1], vh1[q], vl1[q]);
-            else wino_mfma3<false, false>(acc[q][n], cor[q][n], u[q][n][1][0], u[q][n][1][1], vh1[q], vl1[q]);
-            tx_piece(T, 4 * q + n, nrowa, nrowb, 0);
-            if constexpr (FVC_WINO_SB) __builtin_amdgcn_sched_barrier(0);  // keep each gap's work between its MFMA blocks
-          }
-        tx_out(T, vh0, vl0);
-      }
-      wino_mfma_drain(acc, cor);
-      char* const zw = zbuf + zb * kZBytes;
-      combine(zw, acc, cor);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA pieces (rows of the next items)
-      __syncthreads();
-      if (first) nnp = decode(sq[2 + (ntaken & 1)]);  // published by this item's barrier
-      f32x4 rv[2][2];
-      if constexpr (RES) {
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-          for (int j = 0; j < 2; ++j)
-            rv[i][j] = *reinterpret_cast<const f32x4*>(resb + ((size_t)(wave * 4 + i * 2 + j) * 64 + lane) * 16);
-      }
-      finishing(zw, ty, ry, rv);
-
-      // ---- advance
-      if (!nvalid) break;
-      if (!cont) {
-        cur = nxt;
-        nxt = nnp;
-        ++ntaken;
-        row_offsets(cur.g, vo_cur);
-        out_offsets(cur.g);
-        xi_cur = a.x + (size_t)cur.b * ximg_e;
-        yi_cur = a.y + (size_t)cur.b * yimg_e;
-        if constexpr (RES != 0) ri_cur = a.res + (size_t)cur.b * H * W * a.yp;
-      }
-      ty = nty;
-      base = nbase;
-      zb ^= 1;
-    }
-  }
-#else
   if (cur.ty0 < cur.ty1) {
     // first item of the block: its whole 4-row window into ring slots 0..3
     row_offsets(cur.g, vo_cur);
@@ -907,8 +518,29 @@ __global__ __launch_bounds__(256, 1) void conv_wino_kernel(const WinoArgs a) {
       }
       wino_mfma_drain(acc, cor);
 
+      // ---- column combination Z[r][j] = sum_q M[r][q] A[q][j] (M in units of 2^kw: the scale is
+      // applied once on Y) -> LDS plane (r, j, n), lane-linear
       char* const zw = zbuf + zb * kZBytes;
-      combine(zw, acc, cor);
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        f32x4 z0, z1;
+        const f2v ls2 = {1.f / kLoScale, 1.f / kLoScale};
+#pragma unroll
+        for (int cp = 0; cp < 2; ++cp) {
+          f2v m[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const f2v c2 = cp ? f2v{cor[q][n][2], cor[q][n][3]} : f2v{cor[q][n][0], cor[q][n][1]};
+            const f2v a2 = cp ? f2v{acc[q][n][2], acc[q][n][3]} : f2v{acc[q][n][0], acc[q][n][1]};
+            m[q] = __builtin_elementwise_fma(c2, ls2, a2);
+          }
+          const f2v p0 = (m[0] + m[1]) + m[2], p1 = (m[1] - m[2]) - m[3];
+          z0[2 * cp] = p0.x; z0[2 * cp + 1] = p0.y;
+          z1[2 * cp] = p1.x; z1[2 * cp + 1] = p1.y;
+        }
+        *reinterpret_cast<f32x4*>(zw + ((wave * 2 + 0) * 4 + n) * 1024 + lane * 16) = z0;
+        *reinterpret_cast<f32x4*>(zw + ((wave * 2 + 1) * 4 + n) * 1024 + lane * 16) = z1;
+      }
 #if FVC_WINO_KO_WAIT
       asm volatile("" ::: "memory");  // knock-out (experiment builds only): no wait for the next item's rows
 #else
@@ -917,7 +549,112 @@ __global__ __launch_bounds__(256, 1) void conv_wino_kernel(const WinoArgs a) {
       if constexpr (!(FVC_WINO_KO & 4)) __syncthreads();
       if (first) nnp = decode(sq[2 + (ntaken & 1)]);  // published by this item's barrier
 
-      finishing(zw, ty, ry, rv);
+      // ---- finishing pass: wave w -> output channels 16w..16w+15 of the item's 16 tiles
+      if constexpr (!(FVC_WINO_KO & 8)) {
+      f32x4 z[4][2];
+#pragma unroll
+      for (int p = 0; p < 4; ++p)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          if constexpr (FVC_WINO_KO & 32) {
+            z[p][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+            asm volatile("" : "+v"(z[p][j]));
+          } else {
+            z[p][j] = *reinterpret_cast<const f32x4*>(zw + ((p * 2 + j) * 4 + wave) * 1024 + lane * 16);
+          }
+      const f32x4 bj = *reinterpret_cast<const f32x4*>(sbias + cbase);
+      f32x4 yv[2][2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          f32x4 vv;
+#pragma unroll
+          for (int cp = 0; cp < 2; ++cp) {
+            auto pr = [&](const f32x4& x) { return cp ? f2v{x[2], x[3]} : f2v{x[0], x[1]}; };
+            const f2v ys = i == 0 ? (pr(z[0][j]) + pr(z[1][j])) + pr(z[2][j]) : (pr(z[1][j]) - pr(z[2][j])) - pr(z[3][j]);
+            chk2 = __builtin_elementwise_fma(ys, f2v{0.f, 0.f}, chk2);
+            f2v tv = __builtin_elementwise_fma(ys, f2v{a.osc, a.osc}, pr(bj));
+            if constexpr (RES == kResPre) tv += pr(rv[i][j]);
+            if constexpr (ACT == FVC_ACT_RELU) tv = f2v{relu1(tv.x), relu1(tv.y)};
+            if constexpr (ACT == FVC_ACT_LRELU) {
+              const f2v t1 = tv * f2v{0.1f, 0.1f};
+              tv = f2v{fmaxf(tv.x, t1.x), fmaxf(tv.y, t1.y)};
+            }
+            if constexpr (RES == kResPost) tv += pr(rv[i][j]);
+            vv[2 * cp] = tv.x;
+            vv[2 * cp + 1] = tv.y;
+          }
+          yv[i][j] = vv;
+          if constexpr (POST != kPostTap) {
+            if constexpr (FVC_WINO_KO & 16) asm volatile("" ::"v"(vv));
+            else __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, vv), ry, yo[i][j], 0, FVC_STORE_AUX);
+          }
+        }
+      if constexpr (POST == kPostPool) {
+        f32x4 pv;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) pv[c] = (((yv[0][0][c] + yv[0][1][c]) + yv[1][0][c]) + yv[1][1][c]) / 4.f;
+        const __amdgpu_buffer_rsrc_t rp =
+            rsrc(a.pool + ((size_t)cur.b * Hp + ty) * Wp * kC, ty < Hp ? (unsigned)Wp * kC * 4u : 0u);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, pv), rp, po, 0, 0);
+      }
+      if constexpr (POST == kPostTap) {
+        // y never reaches HBM: each wave parks its 16 channels of the item's 64 pixels in its own
+        // planes of this item's Z buffer (no other wave read them), then wave v multiplies the
+        // 64-channel y of pixel (i, j) = (v >> 1, v & 1) of the 16 tiles with the next layer's tap
+        // weights: P [16 partials x 16 tiles] per row tile on v_mfma_f32_16x16x32_f16, split
+        // precision (main = T_hi y_hi, corr = T_lo y_hi + T_hi y_lo), P = main 2^-kt + corr 2^-kt-11.
+        // Z(zb) is next written two items later, behind the next item's barrier.
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            *reinterpret_cast<f32x4*>(zw + ((i * 2 + j) * 4 + wave) * 1024 + lane * 16) = yv[i][j];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) mxy = fmaxf(mxy, fabsf(yv[i][j][c]));
+          }
+        __syncthreads();
+        const int pi = wave >> 1, pj = wave & 1;
+        h8 th[2], tl[2];
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+          // B operand: lane (t, q = lane >> 4) holds channels 32 kk + 8 q .. + 7 of tile t = quads
+          // 2 (q & 1), +1 of wave 2 kk + (q >> 1)
+          const char* src = zw + ((pi * 2 + pj) * 4 + 2 * kk + (lane >> 5)) * 1024 + ((2 * ((lane >> 4) & 1)) * 16 + t) * 16;
+          const f32x4 q0 = *reinterpret_cast<const f32x4*>(src);
+          const f32x4 q1 = *reinterpret_cast<const f32x4*>(src + 256);
+          unsigned hw[4], lw[4];
+          split2(q0[0], q0[1], hw[0], lw[0]);
+          split2(q0[2], q0[3], hw[1], lw[1]);
+          split2(q1[0], q1[1], hw[2], lw[2]);
+          split2(q1[2], q1[3], hw[3], lw[3]);
+          th[kk] = __builtin_bit_cast(h8, v4u{hw[0], hw[1], hw[2], hw[3]});
+          tl[kk] = __builtin_bit_cast(h8, v4u{lw[0], lw[1], lw[2], lw[3]});
+        }
+        const int ox = 32 * cur.g + 2 * t + pj;
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt) {
+          f32x4 pa = {0.f, 0.f, 0.f, 0.f}, pc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int kk = 0; kk < 2; ++kk) {
+            const uint4* const tw = a.tw + (size_t)((rt * 2 + kk) * 2) * 64 + lane;
+            const h8 wh = __builtin_bit_cast(h8, tw[0]);
+            const h8 wl = __builtin_bit_cast(h8, tw[64]);
+            pa = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, th[kk], pa, 0, 0, 0);
+            pc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl, th[kk], pc, 0, 0, 0);
+            pc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, tl[kk], pc, 0, 0, 0);
+          }
+          const int p0 = rt * 16 + 4 * (lane >> 4);
+          f32x4 o;
+#pragma unroll
+          for (int c = 0; c < 4; ++c) o[c] = fmaf(pc[c], a.tosc_c, pa[c] * a.tosc);
+          const unsigned so = (ox < W && p0 < a.pcp) ? (unsigned)((pi * W + ox) * a.pcp + p0) * 4u : kOob;
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, o), ry, so, 0, 0);
+        }
+      }
+
+      }  // FVC_WINO_KO & 8
 
       // ---- advance
       if (!nvalid) break;
@@ -936,7 +673,6 @@ __global__ __launch_bounds__(256, 1) void conv_wino_kernel(const WinoArgs a) {
       zb ^= 1;
     }
   }
-#endif  // FVC_WINO_PIPE
   {
     if ((chk2.x != 0.f || chk2.y != 0.f || !(mxy < 65000.f)) && a.ovf) atomicOr(a.ovf, 1);
   }
