@@ -483,7 +483,7 @@ class GpuGopJob:
         r = {"conv": timer.collect(), "x3": timer.collect(x3=True), "x3_bytes": timer.collect_bytes(x3=True),
              "hbm": timer.collect_hbm(),
              "family": {f: (timer.collect(x3=True, family=f), timer.collect_bytes(x3=True, family=f))
-                        for f in ("x3", "dx", "wino", "wr7")}}
+                        for f in ("x3", "dx", "wino", "wr7", "stem")}}
         if self.args.breakdown:
             for k, (n, ms, fl) in sorted(timer.breakdown().items(), key=lambda kv: -kv[1][1]):
                 print(f"{k:40s} n={n:5d} ms={ms:9.2f} TF/s={fl / (ms * 1e-3) / 1e12:7.2f}", file=sys.stderr)
@@ -699,7 +699,8 @@ def roofline_fields(prof, job, args):
                                "transposed convs, all parity classes per staged tile) + conv_wino_kernel (Winograd "
                                "F(2x2,3x3) for the 64->64 3x3 layers, and the 544x960 128->128 ones as four 64->64 "
                                "quarters) + conv_wr7_kernel (Winograd-rows F(2,7) for SpyNet's 7x7 32->64, 64->32 "
-                               "and 32->16 layers), all their dispatches",
+                               "and 32->16 layers) + conv_stem_kernel (the cin <= 8 stems: Warp_net feature_ext, "
+                               "mvEncoder conv1, resEncoder conv1), all their dispatches",
                      "achieved_is": "algorithmic fp32-conv FLOP (2 x MAC of the direct convolution) / kernel time; "
                                     "the direct kernel issues 3 f16 MFMAs per MAC (ceiling peak/3), the Winograd "
                                     "kernel 3 per 16/36 MAC (ceiling peak/3 x 36/16), the Winograd-rows kernel 3 per "
@@ -726,7 +727,7 @@ def roofline_fields(prof, job, args):
 # f16 MFMA FLOP issued per algorithmic fp32-conv FLOP, per kernel family: 3 split products (hi*hi,
 # hi*lo, lo*hi) per MAC; Winograd F(2x2,3x3) computes 16 products per 36 direct MACs, the
 # Winograd-rows F(2,7) 28 per 49
-ISSUED_PER_FLOP = {"x3": 3.0, "dx": 3.0, "wino": 3.0 * 16.0 / 36.0, "wr7": 3.0 * 28.0 / 49.0}
+ISSUED_PER_FLOP = {"x3": 3.0, "dx": 3.0, "wino": 3.0 * 16.0 / 36.0, "wr7": 3.0 * 28.0 / 49.0, "stem": 3.0}
 
 
 def issued_fields(prof, fam_ms):
@@ -754,7 +755,7 @@ def per_kernel_fields(prof, nfr):
     16/36 of a direct MAC)."""
     out = {}
     for fam, name in (("x3", "conv_x3_kernel"), ("dx", "conv_dx_kernel"), ("wino", "conv_wino_kernel"),
-                      ("wr7", "conv_wr7_kernel")):
+                      ("wr7", "conv_wr7_kernel"), ("stem", "conv_stem_kernel")):
         (ms, fl, n), nbytes = prof["family"][fam]
         if not n:
             continue

@@ -52,6 +52,10 @@ _SIGS = {
     "fvc_conv_wr7_wpack_bytes": (c_size_t, [c_int]),
     "fvc_conv_wr7_pack_weight": (c_int, [vp] + [c_int] * 5 + [vp, vp]),
     "fvc_conv2d_nhwc_wr7": (c_int, [vp, c_int, vp, c_int, c_float, vp, vp] + [c_int] * 7 + [vp, vp, c_int, vp]),
+    "fvc_conv_stem_supported": (c_int, [c_int] * 5),
+    "fvc_conv_stem_wpack_bytes": (c_size_t, [c_int] * 3),
+    "fvc_conv_stem_pack_weight": (c_int, [vp] + [c_int] * 3 + [vp, vp]),
+    "fvc_conv2d_nhwc_stem": (c_int, [vp, vp, c_float, vp, vp] + [c_int] * 8 + [vp, vp]),
     "fvc_wino_tap_wpack_bytes": (c_size_t, [c_int]),
     "fvc_wino_tap_pack_weight": (c_int, [vp, vp, vp, c_int]),
     "fvc_conv2d_nhwc_wino_tap": (c_int, [vp, vp, c_float, vp, vp, vp] + [c_int] * 4 + [vp, c_float, c_int, c_int, vp, vp,

@@ -346,6 +346,16 @@ class PackedConv:
                     _lib.call("fvc_conv_wr7_pack_weight", w.data_ptr(), cin, cout, ci0, co0, nt, up.data_ptr(),
                               ctypes.addressof(uo))
                     self.wr7.append((ci0, co0, nt, mode, up.to(device), float(uo.value)))
+        # small-input stems (cin <= 8 on a 4- or 8-float pixel, cout 64 / 128, 3x3 s1 / s2, 5x5 s2:
+        # Warp_net feature_ext, mvEncoder conv1, resEncoder conv1): the streaming split-precision
+        # kernel (fvc_conv_stem.hip); FVC_STEM=0 keeps the direct x3 kernel (A/B, tests)
+        self.stem = None
+        if (self.x3 and os.environ.get("FVC_STEM", "0") != "0" and
+                bool(lib.fvc_conv_stem_supported(cin, cout, ksize, stride, int(transposed)))):
+            sp = torch.empty(lib.fvc_conv_stem_wpack_bytes(cin, cout, ksize) // 2, dtype=torch.float16)
+            so = ctypes.c_float(0.0)
+            _lib.call("fvc_conv_stem_pack_weight", w.data_ptr(), cin, cout, ksize, sp.data_ptr(), ctypes.addressof(so))
+            self.stem = (sp.to(device), float(so.value))
         # stride-2 transposed layers on the all-classes kernel (fvc_deconv_x3.hip, conv_dx_kernel)
         self.dx = self.x3 and transposed and bool(lib.fvc_deconv_x3_all_classes(cin, cout, ksize, stride))
         if self.x3:
@@ -420,7 +430,12 @@ class PackedConv:
         w128 = (self.wino128 and in_op in (IN_NONE, IN_RELU) and post == POST_NONE and res is None and
                 H * W >= int(os.environ.get("FVC_WINO128_MINPIX", "100000")))
         wr7 = bool(self.wr7) and in_op == IN_NONE and post == POST_NONE and res is None
-        if wr7:
+        stem = self.stem is not None and in_op == IN_NONE and post == POST_NONE and res is None
+        if stem:
+            _lib.call("fvc_conv2d_nhwc_stem", x.data_ptr(), self.stem[0].data_ptr(), self.stem[1], self.bias.data_ptr(),
+                      y.data_ptr(), B, H, W, self.cin, self.cout, self.ksize, self.stride, act,
+                      overflow_flag(x.device).data_ptr(), stream_handle())
+        elif wr7:
             xp, yp = cp4(self.cin), cp4(self.cout)
             for ci0, co0, nt, mode, up, uo in self.wr7:
                 _lib.call("fvc_conv2d_nhwc_wr7", x.data_ptr() + 4 * ci0, xp, up.data_ptr(), nt, uo,
@@ -457,11 +472,11 @@ class PackedConv:
             timer.records.append((ev0, ev1, profiling.conv_flops(self.cin, self.cout, self.ksize, self.stride,
                                                                  self.transposed, B, H, W),
                                   f"{'deconv' if self.transposed else 'conv'}{self.ksize}s{self.stride} "
-                                  f"{self.cin}->{self.cout} @{H}x{W}{' wr7' if wr7 else (' wino' if wino else (' dx' if self.dx else (' x3' if self.x3 else '')))}"
+                                  f"{self.cin}->{self.cout} @{H}x{W}{' stem' if stem else (' wr7' if wr7 else (' wino' if wino else (' dx' if self.dx else (' x3' if self.x3 else ''))))}"
                                   f"{' x4' if w128 else ''}{f' x{len(self.wr7)}' if wr7 and len(self.wr7) > 1 else ''}",
                                   self.x3, nbytes,
-                                  "wr7" if wr7 else ("wino" if wino else ("dx" if self.dx else ("x3" if self.x3 else "f32"))),
-                                  len(self.wr7) if wr7 else 4 if w128 else (1 if wino or not self.x3 else
+                                  "stem" if stem else ("wr7" if wr7 else ("wino" if wino else ("dx" if self.dx else ("x3" if self.x3 else "f32")))),
+                                  len(self.wr7) if wr7 else 4 if w128 else (1 if stem or wino or not self.x3 else
                                                   x3_dispatches(B, 4 * y[0].numel(),
                                                                 4 * res[0].numel() if res is not None else 0))))
         return y

@@ -199,6 +199,20 @@ int fvc_conv2d_nhwc_wr7(const float* x, int xp, const void* upack, int nt, float
                         float* y, int yp, int batch, int h, int w, int mode, int act, int cu_reserve,
                         int* overflow_flag, int* sched, int sched_len, fvc_stream_t stream);
 
+/* Split-precision direct conv for the small-input stems (fvc_conv_stem.hip; replaces ATen conv2d
+ * for DVC/subnet/endecoder.py:253 Warp_net feature_ext 3x3 6->64, analysis_mv.py:19 mvEncoder conv1
+ * 3x3 s2 2->128, analysis.py:15 resEncoder conv1 5x5 s2 3->64): 1 <= cin <= 8 on a 4-float (cin <= 4)
+ * or 8-float pixel, cout 64 / 128, 3x3 s1 / s2 or 5x5 s2, padding k/2, bias + act (none / ReLU /
+ * LeakyReLU 0.1). wpack: fvc_conv_stem_wpack_bytes(cin, cout, k) bytes from fvc_conv_stem_pack_weight
+ * (host; w OIHW). Numerics as fvc_conv2d_nhwc_x3; overflow_flag as there. */
+int fvc_conv_stem_supported(int cin, int cout, int ksize, int stride, int transposed);
+size_t fvc_conv_stem_wpack_bytes(int cin, int cout, int ksize);
+int fvc_conv_stem_pack_weight(const float* w_host, int cin, int cout, int ksize, void* wpack_host,
+                              float* osc_out);
+int fvc_conv2d_nhwc_stem(const float* x, const void* wpack, float osc, const float* bias, float* y,
+                         int batch, int h, int w, int cin, int cout, int ksize, int stride, int act,
+                         int* overflow_flag, fvc_stream_t stream);
+
 /* ------------------------------------------------------------------ layout / resampling */
 int fvc_nchw_to_nhwc(const float* src, float* dst, int batch, int c, int h, int w, int cp,
                      fvc_stream_t stream);

@@ -11,12 +11,12 @@ import argparse
 import csv
 import json
 
-CONV_PREFIXES = ("conv_x3_kernel", "conv_dx_kernel", "conv_wino_kernel", "conv_wr7_kernel", "conv_mfma_f32_kernel",
+CONV_PREFIXES = ("conv_x3_kernel", "conv_dx_kernel", "conv_wino_kernel", "conv_wr7_kernel", "conv_stem_kernel", "conv_mfma_f32_kernel",
                  "conv_mfma_pipe_kernel",
                  "deconv2_mfma_f32_kernel", "conv_smalln_f32_kernel")
 X3 = "conv_x3_kernel"
 WINO = "conv_wino_kernel"
-SPLIT = (X3, "conv_dx_kernel", WINO, "conv_wr7_kernel")  # the split-precision family bench.py's roofline covers
+SPLIT = (X3, "conv_dx_kernel", WINO, "conv_wr7_kernel", "conv_stem_kernel")  # the split-precision family bench.py's roofline covers
 
 
 def is_conv(name):
