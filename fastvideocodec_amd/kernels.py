@@ -350,7 +350,7 @@ class PackedConv:
         # Warp_net feature_ext, mvEncoder conv1, resEncoder conv1): the streaming split-precision
         # kernel (fvc_conv_stem.hip); FVC_STEM=0 keeps the direct x3 kernel (A/B, tests)
         self.stem = None
-        if (self.x3 and os.environ.get("FVC_STEM", "0") != "0" and
+        if (self.x3 and os.environ.get("FVC_STEM", "1") != "0" and
                 bool(lib.fvc_conv_stem_supported(cin, cout, ksize, stride, int(transposed)))):
             sp = torch.empty(lib.fvc_conv_stem_wpack_bytes(cin, cout, ksize) // 2, dtype=torch.float16)
             so = ctypes.c_float(0.0)

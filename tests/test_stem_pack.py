@@ -77,6 +77,6 @@ def test_stem_supported_geometries():
     for cin, cout, k, s in ok:
         assert lib.fvc_conv_stem_supported(cin, cout, k, s, 0) == 1, (cin, cout, k, s)
         assert lib.fvc_conv_stem_wpack_bytes(cin, cout, k) > 0
-    for cin, cout, k, s, tr in [(9, 64, 3, 1, 0), (6, 32, 3, 1, 0), (6, 64, 5, 1, 0), (6, 64, 7, 1, 0),
+    for cin, cout, k, s, tr in [(9, 64, 3, 1, 0), (6, 32, 3, 1, 0), (6, 64, 5, 1, 0), (6, 64, 7, 1, 0), (8, 32, 7, 1, 0),
                                 (6, 64, 3, 2, 1), (0, 64, 3, 1, 0)]:
         assert lib.fvc_conv_stem_supported(cin, cout, k, s, tr) == 0, (cin, cout, k, s, tr)
