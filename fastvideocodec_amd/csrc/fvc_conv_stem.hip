@@ -344,7 +344,11 @@ int fvc_conv_stem_supported(int cin, int cout, int ksize, int stride, int transp
   if (transposed || cin < 1 || cin > 8) return 0;
   // (SpyNet's first layer, 7x7 8 -> 32, ran correctly here in isolation -- tests vs float64 and the
   // direct kernel -- but with it on this kernel the overlapped 8-view / 4K pipelines lost
-  // encoder == decoder bit-exactness at a late P-frame, not root-caused in r5: it stays on x3)
+  // encoder == decoder bit-exactness at a late P-frame, not root-caused in r5: it stays on x3;
+  // -DFVC_STEM_K7 experiment builds re-enable it)
+#ifdef FVC_STEM_K7
+  if (ksize == 7) return cout == 32 && stride == 1;
+#endif
   if (cout != 64 && cout != 128) return 0;
   return (ksize == 3 && (stride == 1 || stride == 2)) || (ksize == 5 && stride == 2);
 }
@@ -434,6 +438,9 @@ int fvc_conv2d_nhwc_stem(const float* x, const void* wpack, float osc, const flo
   if (cinp == 4 && ksize == 5 && stride == 2 && cout == 128) return stem_act<4, 4, 5, 2>(a, act, st);
   if (cinp == 8 && ksize == 5 && stride == 2 && cout == 64) return stem_act<8, 2, 5, 2>(a, act, st);
   if (cinp == 8 && ksize == 5 && stride == 2 && cout == 128) return stem_act<8, 4, 5, 2>(a, act, st);
+#ifdef FVC_STEM_K7
+  if (cinp == 8 && ksize == 7 && stride == 1 && cout == 32) return stem_act<8, 1, 7, 1>(a, act, st);
+#endif
   return FVC_EINVAL;
 }
 

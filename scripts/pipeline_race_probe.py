@@ -1,0 +1,32 @@
+"""Debug aid (r5): encoder recon vs decoder recon of one GOP through the overlapped pipeline and
+the serial one, frame by frame (which frame first differs, by how much, and whether the
+split-precision overflow recompute fired). Run with FVC_LIB_PATH / FVC_* switches to compare."""
+import argparse
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402
+from fastvideocodec_amd import kernels as K  # noqa: E402
+from fastvideocodec_amd.gop import encode_decode_gop  # noqa: E402
+
+dev = torch.device("cuda")
+views = int(os.environ.get("VIEWS", "8"))
+base = dict(gpus=1, steps=1, warmup=0, height=1080, width=1920, gop=3, gops_per_gpu=1, views=0, cpu_baseline="none",
+            json_out=None, breakdown=False, tree=False, serial=False)
+if views > 1:
+    base.update(views=views)
+    job = bench.GpuGopJob(argparse.Namespace(**base), 0, 1, dev)
+else:
+    base.update(height=2160, width=3840, gop=32)
+    job = bench.GpuGopJob(argparse.Namespace(**base), 2, 4, dev)
+for overlap in (True, False):
+    K.x3_overflow(reset=True)
+    job.model.overflow_events = 0
+    bss, dec, _, enc = encode_decode_gop(job.model, job.frames, check=True, overlap=overlap)
+    torch.cuda.synchronize()
+    bad = [(t + 1, float((a - b).abs().max())) for t, (a, b) in enumerate(zip(dec, enc)) if not torch.equal(a, b)]
+    print(f"overlap={overlap}: frames {len(dec)}, mismatching {bad[:5]}, overflow_events "
+          f"{getattr(job.model, 'overflow_events', 0)}, precisions {sorted(set(b.precision for b in bss))}", flush=True)

@@ -110,3 +110,28 @@ def test_stem_rejects_unsupported(dev):
     assert lib.fvc_conv_stem_supported(6, 32, 3, 1, 0) == 0   # cout
     assert lib.fvc_conv_stem_supported(6, 64, 5, 1, 0) == 0   # 5x5 stride 1
     assert lib.fvc_conv_stem_supported(6, 64, 3, 2, 1) == 0   # transposed
+
+
+@pytest.mark.parametrize("case", [(6, 64, 3, 1, K.ACT_RELU), (2, 128, 3, 2, K.ACT_LRELU), (3, 64, 5, 2, K.ACT_NONE)],
+                         ids=["feature_ext", "mvEncoder_conv1", "resEncoder_conv1"])
+def test_stem_full_size_matches_direct(dev, case):
+    """The production geometries at 1088x1920, two frames (thousands of tiles per launch, every
+    persistent block looping over many): equal to the direct x3 kernel within the two kernels'
+    rounding (both ~2e-7 of scale from float64), deterministic, no overflow."""
+    cin, cout, k, s, act = case
+    g = torch.Generator().manual_seed(11 + cin)
+    w = torch.randn(cout, cin, k, k, generator=g) * (1.0 / (cin * k * k) ** 0.5)
+    b = torch.randn(cout, generator=g) * 0.1
+    ps, pd = _packs(dev, w, b, s)
+    x = torch.rand(2, 1088, 1920, K.cp4(cin), generator=g)
+    x[..., cin:] = 0.0
+    xd = x.to(dev)
+    K.x3_overflow(reset=True)
+    ys, yd = ps(xd, act=act), pd(xd, act=act)
+    ys2 = ps(xd, act=act)
+    torch.cuda.synchronize()
+    assert not K.x3_overflow(reset=True)
+    assert torch.equal(ys, ys2)
+    scale = float(yd.abs().max())
+    diff = float((ys - yd).abs().max()) / scale
+    assert diff <= 1e-6, diff
