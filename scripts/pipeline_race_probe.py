@@ -30,3 +30,22 @@ for overlap in (True, False):
     bad = [(t + 1, float((a - b).abs().max())) for t, (a, b) in enumerate(zip(dec, enc)) if not torch.equal(a, b)]
     print(f"overlap={overlap}: frames {len(dec)}, mismatching {bad[:5]}, overflow_events "
           f"{getattr(job.model, 'overflow_events', 0)}, precisions {sorted(set(b.precision for b in bss))}", flush=True)
+
+# where does the overlapped run diverge? re-decode every bitstream serially and rebuild the
+# decoder chain from the pipeline's own previous decoded frame
+if os.environ.get("LOCATE", "0") == "1":
+    K.x3_overflow(reset=True)
+    bss, dec, _, enc = encode_decode_gop(job.model, job.frames, check=True, overlap=True)
+    torch.cuda.synchronize()
+    x_prev = job.frames[:, 0].contiguous()
+    with torch.no_grad():
+        for t, bs in enumerate(bss, 1):
+            dl = job.model.decode_latents(bs, check=True)
+            r = job.model.reconstruct(dl, x_prev)
+            torch.cuda.synchronize()
+            print(f"t={t}: serial(bs, pipeline dec[t-1]) == pipeline dec[t]: {torch.equal(r, dec[t - 1])}, "
+                  f"== enc[t]: {torch.equal(r, enc[t - 1])}; pipeline dec == enc: {torch.equal(dec[t - 1], enc[t - 1])}",
+                  flush=True)
+            x_prev = dec[t - 1]
+            if t >= 8:
+                break
