@@ -304,7 +304,7 @@ if os.environ.get("LOCATE", "0") == "6":
 # LOCATE=6's reads before the kernel hid it. LOCATE=7 keeps LOCATE=5's timing (checksums only
 # AFTER each reconstruction op) and, after the warp/assemble kernel, also copies its inputs and
 # output: a wrong output next to unchanged inputs means the kernel read wrong data
-if os.environ.get("LOCATE", "0") in ("7", "8"):
+if os.environ.get("LOCATE", "0") in ("7", "8", "9"):
     m = job.model
     state = {"in_rec": False}
     sums, mcrec = [], []
@@ -454,3 +454,26 @@ if os.environ.get("LOCATE", "0") in ("7", "8"):
                 zt = sorted(set(zt))
                 print(f"  zero-read tap pixels (flat, first 24): {zt[:24]}; 16-B pixel -> 128-B line: "
                       f"{sorted(set(v // 8 for v in zt))[:24]}", flush=True)
+
+    # LOCATE=9: is a wrong pixel exactly the warp of this frame's reference by an EARLIER frame's
+    # flow (a stale flow read), or of an earlier frame's reference by this frame's flow?
+    if os.environ["LOCATE"] == "9":
+        shown = 0
+        for t, r in enumerate(mcrec):
+            if shown >= 6:
+                break
+            wf2, _ = mc(r["ref"], r["mv"])
+            torch.cuda.synchronize()
+            d = (wf2 != r["wf"]).any(-1)
+            if not bool(d.any()):
+                continue
+            n = int(d.sum())
+            got_f, got_r = torch.zeros_like(d), torch.zeros_like(d)
+            shown += 1
+            for u in range(max(0, t - 6), t):
+                wu, _ = mc(r["ref"], mcrec[u]["mv"])
+                got_f |= d & (wu == r["wf"]).all(-1)
+                wu, _ = mc(mcrec[u]["ref"], r["mv"])
+                got_r |= d & (wu == r["wf"]).all(-1)
+            print(f"frame {t}: {n} wrong px; = this ref warped by an earlier frame's flow: {int(got_f.sum())}; "
+                  f"= an earlier ref warped by this flow: {int(got_r.sum())}", flush=True)
