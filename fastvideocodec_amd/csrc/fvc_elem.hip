@@ -428,6 +428,65 @@ __global__ void k_up2_add_q16(const float* __restrict__ src, const float* __rest
   }
 }
 
+// NE elements per thread per iteration (e, e + stride, ...), all loads issued before the stores:
+// more independent loads in flight per wave than the one-element loop (as k_mc_assemble_q); NT:
+// the skip tensor by non-temporal loads (it is read once)
+template <bool NT>
+__device__ __forceinline__ float4 up2_q16_elem(const float4* __restrict__ s4, const float* __restrict__ skip,
+                                               unsigned e, unsigned H, unsigned W, int h, int w, int ac, float scale,
+                                               unsigned mW, unsigned mH) {
+  const unsigned c4 = e & 15u;
+  const unsigned p = e >> 4;
+  const unsigned row = udiv_magic(p, W, mW);
+  const int x = (int)(p - row * W);
+  const unsigned b = udiv_magic(row, H, mH);
+  const int y = (int)(row - b * H);
+  const UpIdx uy = up_index(y, h, (int)H, ac), ux = up_index(x, w, (int)W, ac);
+  const unsigned bb = b * (unsigned)h * (unsigned)w;
+  const float4 a = s4[(bb + (unsigned)uy.i0 * w + ux.i0) * 16u + c4];
+  const float4 bq = s4[(bb + (unsigned)uy.i0 * w + ux.i1) * 16u + c4];
+  const float4 c = s4[(bb + (unsigned)uy.i1 * w + ux.i0) * 16u + c4];
+  const float4 d = s4[(bb + (unsigned)uy.i1 * w + ux.i1) * 16u + c4];
+  float4 v;
+  v.x = (a.x * ux.l0 + bq.x * ux.l1) * uy.l0 + (c.x * ux.l0 + d.x * ux.l1) * uy.l1;
+  v.y = (a.y * ux.l0 + bq.y * ux.l1) * uy.l0 + (c.y * ux.l0 + d.y * ux.l1) * uy.l1;
+  v.z = (a.z * ux.l0 + bq.z * ux.l1) * uy.l0 + (c.z * ux.l0 + d.z * ux.l1) * uy.l1;
+  v.w = (a.w * ux.l0 + bq.w * ux.l1) * uy.l0 + (c.w * ux.l0 + d.w * ux.l1) * uy.l1;
+  if (scale != 1.f) { v.x *= scale; v.y *= scale; v.z *= scale; v.w *= scale; }
+  if (skip) {
+    float4 sk;
+    if constexpr (NT) {
+      const float* q = skip + 4 * (size_t)e;
+      sk = make_float4(__builtin_nontemporal_load(q), __builtin_nontemporal_load(q + 1), __builtin_nontemporal_load(q + 2),
+                       __builtin_nontemporal_load(q + 3));
+    } else {
+      sk = reinterpret_cast<const float4*>(skip)[e];
+    }
+    v.x = sk.x + v.x; v.y = sk.y + v.y; v.z = sk.z + v.z; v.w = sk.w + v.w;
+  }
+  return v;
+}
+
+template <int NE, bool NT>
+__global__ void k_up2_add_q16p(const float* __restrict__ src, const float* __restrict__ skip, float* __restrict__ out,
+                               int B, int h, int w, int ac, float scale, unsigned mW, unsigned mH) {
+  const unsigned H = 2u * h, W = 2u * w;
+  const unsigned n = (unsigned)B * H * W * 16u;
+  const unsigned st = gridDim.x * blockDim.x;
+  const float4* s4 = reinterpret_cast<const float4*>(src);
+  for (unsigned e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += NE * st) {
+    unsigned ei[NE];
+    float4 v[NE];
+#pragma unroll
+    for (int k = 0; k < NE; ++k) {
+      ei[k] = e + k * st < n ? e + k * st : e;
+      v[k] = up2_q16_elem<NT>(s4, skip, ei[k], H, W, h, w, ac, scale, mW, mH);
+    }
+#pragma unroll
+    for (int k = 0; k < NE; ++k) reinterpret_cast<float4*>(out)[ei[k]] = v[k];
+  }
+}
+
 __global__ void k_up2_add(const float* __restrict__ src, const float* __restrict__ skip, float* __restrict__ out,
                           int B, int h, int w, int cp, int ac, float scale) {
   const int H = 2 * h, W = 2 * w, c4n = cp / 4;
@@ -1362,8 +1421,19 @@ int fvc_upsample2x_add_nhwc(const float* src, const float* skip, float* out, int
   const unsigned long long H2 = 2ull * h, W2 = 2ull * w;
   if (cp == 64 && (unsigned long long)batch * H2 * W2 * 16ull < (1ull << 32) && env_flag("FVC_UP2_Q16", 1)) {
     const unsigned mW = (unsigned)(((1ull << 32) + W2 - 1) / W2), mH = (unsigned)(((1ull << 32) + H2 - 1) / H2);
-    hipLaunchKernelGGL(k_up2_add_q16, dim3(grid_for(n)), dim3(kBlk), 0, (hipStream_t)s, src, skip, out, batch, h, w,
-                       align_corners, scale, mW, mH);
+    // (index arithmetic e + 2 * stride stays below 2^32: stride <= 8192 * kBlk)
+    // two elements per thread, the skip tensor (read once: c0 / c1 are dead after this add) by
+    // non-temporal loads: 1088x1920x64 at 8 frames 2.16 -> 1.99 ms (profiles/r5/up2_pair); same bits
+    const bool nt = env_flag("FVC_UP2_NT", 1) != 0;
+    if (n + (1ull << 24) < (1ull << 32) && env_flag("FVC_UP2_PAIR", 1) && nt)
+      hipLaunchKernelGGL((k_up2_add_q16p<2, true>), dim3(grid_for((n + 1) / 2)), dim3(kBlk), 0, (hipStream_t)s, src, skip,
+                         out, batch, h, w, align_corners, scale, mW, mH);
+    else if (n + (1ull << 24) < (1ull << 32) && env_flag("FVC_UP2_PAIR", 1))
+      hipLaunchKernelGGL((k_up2_add_q16p<2, false>), dim3(grid_for((n + 1) / 2)), dim3(kBlk), 0, (hipStream_t)s, src, skip,
+                         out, batch, h, w, align_corners, scale, mW, mH);
+    else
+      hipLaunchKernelGGL(k_up2_add_q16, dim3(grid_for(n)), dim3(kBlk), 0, (hipStream_t)s, src, skip, out, batch, h, w,
+                         align_corners, scale, mW, mH);
   } else {
     hipLaunchKernelGGL(k_up2_add, dim3(grid_for(n)), dim3(kBlk), 0, (hipStream_t)s, src, skip, out, batch, h, w, cp,
                        align_corners, scale);
