@@ -10,7 +10,8 @@ import sys
 from concurrent.futures import ThreadPoolExecutor
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-VARIANT_SRCS = ("fvc_conv_x3.hip", "fvc_deconv_x3.hip", "fvc_conv_wino.hip", "fvc_conv_wr7.hip", "fvc_conv_stem.hip")
+VARIANT_SRCS = ("fvc_conv_x3.hip", "fvc_deconv_x3.hip", "fvc_conv_wino.hip", "fvc_conv_wr7.hip", "fvc_conv_stem.hip",
+                "fvc_elem.hip")
 SRCS = ["fvc_conv.hip", "fvc_conv_x3.hip", "fvc_deconv_x3.hip", "fvc_conv_wino.hip", "fvc_conv_wr7.hip", "fvc_conv_stem.hip", "fvc_elem.hip", "fvc_coder.hip", "fvc_iframe.hip",
         "fvc_torchac.hip"]
 # per-source flags: the Winograd transforms stay scalar f32 (packed f32 VALU issues slower beside MFMAs)

@@ -46,7 +46,7 @@ struct StemArgs {
   const uint4* w;     // [step][n][plane][lane] 16-B fragments
   const float* bias;  // [cout]
   float* y;           // [B][Ho][Wo][cout]
-  int B, H, W, Ho, Wo, cout;
+  int B, H, W, Ho, Wo, cin, cout;
   int tiles_x, tiles_y, ntiles;
   float osc, osc_c;
   int* ovf;
@@ -155,6 +155,11 @@ __global__ __launch_bounds__(64 * NW) void conv_stem_kernel(const StemArgs a) {
       const bool ok = e < T::kItems && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
       const unsigned off = ok ? (unsigned)((iy * W + ix) * CINP + 4 * qd) * 4u : kOob;
       v[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rx, off, 0, 0));
+      // the pad channels (cin .. CINP-1) are masked here rather than trusted to be zero: their
+      // weights are 0, but a NaN / Inf a producer left there would turn 0 * x into NaN
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (4 * qd + i >= a.cin) v[j][i] = 0.f;
     }
   };
   auto stage = [&](int buf) {
@@ -415,6 +420,7 @@ int fvc_conv2d_nhwc_stem(const float* x, const void* wpack, float osc, const flo
   a.W = w;
   a.Ho = h / stride;
   a.Wo = w / stride;
+  a.cin = cin;
   a.cout = cout;
   if ((unsigned long long)batch * a.Ho * a.Wo * cout >= (1ull << 32)) return FVC_EINVAL;
   a.tiles_x = fvc_cdiv(a.Wo, 32);

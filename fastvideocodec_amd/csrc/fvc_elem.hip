@@ -635,20 +635,66 @@ __global__ void k_mc_assemble_q(const float* __restrict__ ref, const float* __re
   const unsigned npix = (unsigned)B * H * W;
   const unsigned st = gridDim.x * blockDim.x;
   const float4* const r4 = reinterpret_cast<const float4*>(ref);
+#if defined(FVC_MC_ACQ)
+  // experiment (r6 race probe): an agent-scope acquire (this CU's L1 invalidated) before any load
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+#endif
+#if defined(FVC_MC_SC1) || defined(FVC_MC_BUF)
+  // experiment (r6 race probe): every load of the kernel as a buffer load; FVC_MC_SC1 sets sc1
+  // (bypasses the CU's L1, served by the XCD's L2), FVC_MC_BUF is the plain-policy control
+#if defined(FVC_MC_SC1)
+  constexpr int kAux = 16;
+#else
+  constexpr int kAux = 0;
+#endif
+  const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc((void*)ref, (short)0, (int)(npix * 16u), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rm = __builtin_amdgcn_make_buffer_rsrc((void*)mv, (short)0, (int)(npix * 16u), 0x00020000);
+  auto ld = [&](const __amdgpu_buffer_rsrc_t& r, unsigned px) -> float4 {
+    return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, px * 16u, 0, kAux));
+  };
+  auto sample = [&](unsigned bbase, const WarpTap& t) -> float4 {
+    const unsigned r0 = bbase + (unsigned)t.y0 * W + t.x0;
+    const unsigned dx = t.vx1 ? 1u : 0u, dy = t.vy1 ? (unsigned)W : 0u;
+#if defined(FVC_MC_NEFIRST)
+    // the east taps' loads issued before the west taps' (each pair shares its lines)
+    const float4 vne = ld(rr, r0 + dx), vse = ld(rr, r0 + dy + dx);
+    __builtin_amdgcn_sched_barrier(0);
+    const float4 vnw = ld(rr, r0), vsw = ld(rr, r0 + dy);
+#else
+    const float4 vnw = ld(rr, r0), vne = ld(rr, r0 + dx), vsw = ld(rr, r0 + dy), vse = ld(rr, r0 + dy + dx);
+#endif
+    float4 o;
+    o.x = ((vnw.x * t.nw + vne.x * t.ne) + vsw.x * t.sw) + vse.x * t.se;
+    o.y = ((vnw.y * t.nw + vne.y * t.ne) + vsw.y * t.sw) + vse.y * t.se;
+    o.z = ((vnw.z * t.nw + vne.z * t.ne) + vsw.z * t.sw) + vse.z * t.se;
+    o.w = ((vnw.w * t.nw + vne.w * t.ne) + vsw.w * t.sw) + vse.w * t.se;
+    return o;
+  };
+#endif
   // two pixels per iteration, all loads of both issued before either's stores: the gathers depend
   // on the flow load (two dependent HBM round trips per pixel), so latency, not bytes, bounds a
   // one-pixel loop
   for (unsigned p = blockIdx.x * blockDim.x + threadIdx.x; p < npix; p += 2 * st) {
     const unsigned p2 = p + st < npix ? p + st : p;
+#if defined(FVC_MC_SC1) || defined(FVC_MC_BUF)
+    const float4 f1 = ld(rm, p), f2 = ld(rm, p2);
+    const float4 r1 = ld(rr, p), r2 = ld(rr, p2);
+#else
     const float4 f1 = reinterpret_cast<const float4*>(mv)[p];
     const float4 f2 = reinterpret_cast<const float4*>(mv)[p2];
     const float4 r1 = r4[p], r2 = r4[p2];
+#endif
     const unsigned row1 = udiv_magic(p, W, mW), b1 = udiv_magic(row1, H, mH);
     const unsigned row2 = udiv_magic(p2, W, mW), b2 = udiv_magic(row2, H, mH);
     const WarpTap t1 = warp_tap((int)(row1 - b1 * H), (int)(p - row1 * W), f1.x, f1.y, H, W);
     const WarpTap t2 = warp_tap((int)(row2 - b2 * H), (int)(p2 - row2 * W), f2.x, f2.y, H, W);
+#if defined(FVC_MC_SC1) || defined(FVC_MC_BUF)
+    float4 w1 = sample(b1 * H * W, t1);
+    float4 w2 = sample(b2 * H * W, t2);
+#else
     float4 w1 = warp_sample4_nb(r4, b1 * H * W, W, H, t1);
     float4 w2 = warp_sample4_nb(r4, b2 * H * W, W, H, t2);
+#endif
     w1.w = 0.f;
     w2.w = 0.f;
     float4* const wf = reinterpret_cast<float4*>(warpframe);

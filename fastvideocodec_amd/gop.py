@@ -31,7 +31,7 @@ from . import kernels as K
 # CUs the conv kernels' persistent grids leave free while the pipeline's side streams run.
 # r1 (static schedule, 4 GOPs per step, scripts/gpu_reserve_sweep.sh): 16 -> 49.2, 24 -> 50.3,
 # 32 -> 51.1, 40 -> 50.4, 48 -> 49.4, 64 -> 48.7 P-frames/s. r4 (dynamic work-item schedule,
-# segment-framed rANS with short chains, 16 GOPs, scripts/gpu_reserve_sweep_r4.sh, two runs each):
+# segment-framed rANS with short chains, 16 GOPs, two runs each; data in profiles/r4/reserve_sweep/):
 # 32 -> 71.13 / 71.00, 16 -> 71.79 / 71.68, 8 -> 72.27 / 72.37, 0 -> 72.49 / 72.56: no reserve.
 PIPELINE_CU_RESERVE = int(os.environ.get("FVC_PIPELINE_CU_RESERVE", "0"))
 

@@ -386,10 +386,11 @@ class PackedConv:
             return
         now = int(_lib.load().fvc_conv_x3_layout_id(self.cin, self.cout, self.ksize, self.stride,
                                                       int(self.transposed)))
-        self._layout_env = env
         if now != self.layout:
             raise _lib.FvcError("x3 weight pack was built under another layout configuration (an FVC_DX / "
                                 "FVC_X3_* switch changed since packing); re-create the PackedConv")
+        # cached only once the check has passed: a refused env must be refused on every call
+        self._layout_env = env
 
     def out_hw(self, h, w):
         if self.transposed:

@@ -477,3 +477,145 @@ if os.environ.get("LOCATE", "0") in ("7", "8", "9"):
                 got_r |= d & (wu == r["wf"]).all(-1)
             print(f"frame {t}: {n} wrong px; = this ref warped by an earlier frame's flow: {int(got_f.sum())}; "
                   f"= an earlier ref warped by this flow: {int(got_r.sum())}", flush=True)
+
+# LOCATE=10 (r6): LOCATE=7's timing, plus (a) the pointer range and stream of every conv / HBM op
+# of every stream while the GOP runs, and (b) per wrong pixel of the first bad frames: the flow,
+# the four taps (pixel index, byte address, bilinear weight, the value memory holds), the wrong and
+# the right output, and which single-cause models reproduce the wrong value: a tap read as zeros
+# (any subset, whole 16 B), a dword read as zero (per channel), a zero flow component. Written to
+# gpurun_out/race10_<tag>.json for offline analysis.
+if os.environ.get("LOCATE", "0") == "10":
+    import itertools
+    import json
+    import numpy as np
+    m = job.model
+    state = {"in_rec": False, "frame": -1}
+    mcrec, opsrec = [], []
+
+    def _tensors(o):
+        if torch.is_tensor(o):
+            return [o]
+        if isinstance(o, (tuple, list)):
+            return [t for v in o for t in _tensors(v)]
+        return []
+
+    def rng(t):
+        return [t.data_ptr(), t.data_ptr() + t.numel() * t.element_size()]
+
+    def ck(name, fn):
+        def w(*a, **kw):
+            out = fn(*a, **kw)
+            sid = torch.cuda.current_stream().cuda_stream
+            ins = [rng(t) for t in _tensors(list(a)) if t.is_cuda]
+            outs = [rng(t) for t in _tensors(out) if t.is_cuda]
+            opsrec.append(dict(name=name, stream=sid, rec=state["in_rec"], frame=state["frame"], ins=ins, outs=outs))
+            if state["in_rec"] and name == "mc_assemble":
+                ref, mv = a
+                mcrec.append(dict(ref=ref.clone(), mv=mv.clone(), wf=out[0].clone(), frame=state["frame"],
+                                  op_index=len(opsrec) - 1, ptr=ref.data_ptr()))
+            return out
+        return w
+
+    orig_rec = m.reconstruct
+
+    def rec_wrap(lat, referframe):
+        state["frame"] += 1
+        state["in_rec"] = True
+        try:
+            return orig_rec(lat, referframe)
+        finally:
+            state["in_rec"] = False
+
+    patches = [(K.PackedConv, "__call__"), (K.PackedConv, "call_pool"), (K.PackedConv, "call_tap"),
+               (K.TapConsumer, "gather"), (K, "upsample2x_add"), (K, "mc_assemble"), (K, "nchw_to_nhwc"),
+               (K, "spynet_assemble"), (K, "avgpool2")]
+    saved_fns = [(o, n, getattr(o, n)) for o, n in patches]
+    for o, n, f in saved_fns:
+        setattr(o, n, ck(n, f))
+    m.reconstruct = rec_wrap
+    K.x3_overflow(reset=True)
+    bss, dec, _, enc = encode_decode_gop(m, job.frames, check=True, overlap=True)
+    torch.cuda.synchronize()
+    m.reconstruct = orig_rec
+    for o, n, f in saved_fns:
+        setattr(o, n, f)
+    bad = [t for t, (a, b) in enumerate(zip(dec, enc)) if not torch.equal(a, b)]
+    print("decoder mismatching frames (0-based):", bad[:8], flush=True)
+    mc = K.mc_assemble
+    report = dict(lib=os.environ.get("FVC_LIB_PATH", "product"), bad=bad[:16], frames=[])
+    summary = {"px": 0, "zero_tap": 0, "zero_dword": 0, "flow0": 0, "unexplained": 0}
+    for r in mcrec[:8]:
+        wf2, _ = mc(r["ref"], r["mv"])
+        torch.cuda.synchronize()
+        d = (wf2 != r["wf"]).any(-1)[0]
+        if not bool(d.any()):
+            continue
+        ref = r["ref"][0].double().cpu().numpy()
+        mvv = r["mv"][0].double().cpu().numpy()
+        wrong = r["wf"][0].double().cpu().numpy()
+        right = wf2[0].double().cpu().numpy()
+        H, W = d.shape
+        ys, xs = [v.cpu().numpy() for v in torch.nonzero(d, as_tuple=True)]
+        base = r["ptr"]
+        # ops of any stream launched between the previous reconstruct's mc and this one (program order)
+        lo = max([q["op_index"] for q in mcrec if q["op_index"] < r["op_index"]] + [0])
+        window = [dict(name=o["name"], stream=o["stream"], rec=o["rec"], ins=o["ins"], outs=o["outs"])
+                  for o in opsrec[lo:r["op_index"] + 1]]
+        pxs = []
+        for y, x in zip(ys, xs):
+            fx, fy = mvv[y, x, 0], mvv[y, x, 1]
+
+            def taps_of(fx, fy):
+                gx = (-1.0 + 2.0 * x / (W - 1)) + fx / ((W - 1) / 2.0)
+                gy = (-1.0 + 2.0 * y / (H - 1)) + fy / ((H - 1) / 2.0)
+                ix = min(max((gx + 1) * W / 2 - 0.5, 0.0), W - 1.0)
+                iy = min(max((gy + 1) * H / 2 - 0.5, 0.0), H - 1.0)
+                x0, y0 = int(np.floor(ix)), int(np.floor(iy))
+                ax, ay = ix - x0, iy - y0
+                tt = [(y0, x0, (1 - ax) * (1 - ay)), (y0, x0 + 1, ax * (1 - ay)), (y0 + 1, x0, (1 - ax) * ay),
+                      (y0 + 1, x0 + 1, ax * ay)]
+                return [(a, b, w) for a, b, w in tt if a < H and b < W]
+
+            taps = taps_of(fx, fy)
+            tol = 2e-5
+            z_tap = any(np.abs(sum(w * (0.0 if mk else ref[a, b, :3]) for (a, b, w), mk in zip(taps, mask))
+                               - wrong[y, x, :3]).max() < tol
+                        for mask in itertools.product((0, 1), repeat=len(taps)) if any(mask))
+            z_dw = all(any(abs(sum(w * (0.0 if mk else ref[a, b, c]) for (a, b, w), mk in zip(taps, mask))
+                               - wrong[y, x, c]) < tol for mask in itertools.product((0, 1), repeat=len(taps)))
+                       for c in range(3))
+            f0 = False
+            for gfx, gfy in ((0.0, 0.0), (0.0, fy), (fx, 0.0)):
+                tq = taps_of(gfx, gfy)
+                if np.abs(sum(w * ref[a, b, :3] for a, b, w in tq) - wrong[y, x, :3]).max() < tol:
+                    f0 = True
+            summary["px"] += 1
+            summary["zero_tap"] += z_tap
+            summary["zero_dword"] += z_dw
+            summary["flow0"] += f0
+            summary["unexplained"] += not (z_tap or z_dw or f0)
+            if len(pxs) < 24:
+                pxs.append(dict(y=int(y), x=int(x), flow=[fx, fy],
+                                taps=[dict(y=a, x=b, w=w, addr=base + 16 * (a * W + b),
+                                           val=ref[a, b, :3].tolist()) for a, b, w in taps],
+                                wrong=wrong[y, x, :3].tolist(), right=right[y, x, :3].tolist(),
+                                zero_tap=bool(z_tap), zero_dword=bool(z_dw), flow0=bool(f0)))
+        # which ranges of other-stream ops hold any wrong tap's address?
+        hits = {}
+        for pxd in pxs:
+            for tp in pxd["taps"]:
+                for o in window:
+                    for kind in ("ins", "outs"):
+                        for lo_, hi_ in o[kind]:
+                            if lo_ <= tp["addr"] < hi_ and not (o["rec"] and o["name"] in ("mc_assemble", "nchw_to_nhwc")):
+                                key = f"{o['name']}:{kind}:stream{o['stream']}:rec{int(o['rec'])}"
+                                hits[key] = hits.get(key, 0) + 1
+        fr = dict(frame=r["frame"], wrong_px=int(d.sum()), ref_range=[base, base + r["ref"].numel() * 4],
+                  pixels=pxs, alias_hits=hits, window=window)
+        report["frames"].append(fr)
+        print(f"frame {r['frame']}: {int(d.sum())} wrong px; alias hits {hits}", flush=True)
+    print("summary (per wrong pixel, single-cause models):", summary, flush=True)
+    report["summary"] = summary
+    os.makedirs("gpurun_out", exist_ok=True)
+    with open(f"gpurun_out/race10_{os.environ.get('TAG', 'x')}.json", "w") as f:
+        json.dump(report, f)

@@ -3,7 +3,7 @@
 bench.py's roofline object (which times the split-precision conv kernels -- conv_x3_kernel and
 conv_wino_kernel -- with HIP events on their stream).
 
-usage: python scripts/rocprof_summary.py <stats_csv> <n_pframes_total>
+usage: python scripts/rocprof_summary.py <stats_csv> --bench-json bench_serial.json
            [--fetch fetch_counter_collection.csv --write write_counter_collection.csv
             --json-out profiles/r1/x3_traffic.json --height 1080 --width 1920]
 """
@@ -36,7 +36,10 @@ def pmc_per_dispatch(path, counter, sub):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("stats")
-    ap.add_argument("nframes", type=int)
+    ap.add_argument("nframes", type=int, nargs="?", default=None,
+                    help="P-frames the trace covers (default: derived from --bench-json and the launch count)")
+    ap.add_argument("--bench-json", help="the profiled command's bench JSON: per-kernel launches and P-frames "
+                    "per serial pass, so the P-frame count is derived from the trace's own launch count")
     ap.add_argument("--fetch")
     ap.add_argument("--write")
     ap.add_argument("--json-out")
@@ -44,8 +47,25 @@ def main():
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--gops-per-gpu", type=int, default=16, help="the profiled bench's GOPs per step")
     a = ap.parse_args()
-    nframes = a.nframes
     rows = list(csv.DictReader(open(a.stats)))
+    nframes = a.nframes
+    if a.bench_json:
+        # the trace may hold several serial passes (warm-up + timed); the P-frames it
+        # covers = (split-family launches in the trace / launches per pass) x P-frames per pass
+        b = json.load(open(a.bench_json))
+        per_pass = sum(v["launches"] for k, v in b["roofline"]["per_kernel"].items() if k in SPLIT)
+        pf_pass = round(b["value"] * b["ms_per_step"] / 1000.0 / b["n_gpus"])  # one rank's P-frames per step
+        traced = sum(int(r["Calls"]) for r in rows if any(x in r["Name"] for x in SPLIT))
+        if traced % per_pass:
+            raise SystemExit(f"trace holds {traced} split launches, not a multiple of {per_pass} per pass")
+        derived = traced // per_pass * pf_pass
+        print(f"P-frames traced: {traced} split-family launches / {per_pass} per pass = {traced // per_pass} "
+              f"passes x {pf_pass} P-frames = {derived}")
+        if nframes is not None and nframes != derived:
+            print(f"  (the given count {nframes} disagrees with the trace; using {derived})")
+        nframes = derived
+    if nframes is None:
+        raise SystemExit("give the P-frame count or --bench-json")
     tot = sum(float(r["TotalDurationNs"]) for r in rows)
     conv = sum(float(r["TotalDurationNs"]) for r in rows if is_conv(r["Name"]))
     calls = sum(int(r["Calls"]) for r in rows if is_conv(r["Name"]))

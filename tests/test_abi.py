@@ -225,6 +225,24 @@ def test_x3_layout_id_tracks_layout_switches(monkeypatch):
     assert lib.fvc_conv_x3_layout_id(3, 64, 5, 2, 0) == 0  # back on the fp32 kernels
 
 
+def test_layout_check_refuses_on_every_call(monkeypatch):
+    """PackedConv._check_layout caches the env snapshot it last accepted; a snapshot it
+    refused must be refused again on the next call, not remembered as checked."""
+    from fastvideocodec_amd import kernels as K
+    for k in K._LAYOUT_ENV:
+        monkeypatch.delenv(k, raising=False)
+    pc = object.__new__(K.PackedConv)  # host-side state only: no device pack needed for the check
+    pc.cin, pc.cout, pc.ksize, pc.stride, pc.transposed = 128, 128, 3, 2, True
+    pc.layout = int(_lib.load().fvc_conv_x3_layout_id(128, 128, 3, 2, 1))
+    pc._check_layout()
+    monkeypatch.setenv("FVC_DX", "0")
+    for _ in range(3):
+        with pytest.raises(_lib.FvcError):
+            pc._check_layout()
+    monkeypatch.setenv("FVC_DX", "1")
+    pc._check_layout()
+
+
 def test_segment_framing_rows():
     """'segment' framing (the codec's default stream cut): >= 512 symbols per stream, a power-of-two
     count of equal contiguous segments per (frame, channel) row; the other framings unchanged."""

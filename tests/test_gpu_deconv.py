@@ -150,6 +150,8 @@ def test_pack_layout_switch_refused(dev, monkeypatch):
     monkeypatch.setenv("FVC_DX", "0")
     with pytest.raises(_lib.FvcError):
         pc(x)
+    with pytest.raises(_lib.FvcError):  # and again: the refusal is not cached away
+        pc(x)
     monkeypatch.setenv("FVC_DX", "1")
     b = pc(x)
     torch.cuda.synchronize()

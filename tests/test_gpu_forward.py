@@ -420,3 +420,7 @@ def test_gop12_1080p_closed_loop_vs_reference(model, dev):
     assert max(dbpp[1:]) <= 2 * max(max(v[1:]) for v in rb.values()), dbpp
     assert np.mean(drift[1:]) <= 2 * max(np.mean(v[1:]) for v in rp.values()), drift
     assert np.mean(dbpp[1:]) <= 2 * max(np.mean(v[1:]) for v in rb.values()), dbpp
+    # fixed ceilings, independent of the fixture: a regenerated fixture with a wider
+    # reference spread cannot widen the gate past them (the committed fixture's 2x envelope is
+    # 1.4e-2 dB and 1.9e-3 relative bpp, so they do not bind today)
+    assert max(drift) <= 2e-2 and max(dbpp) <= 2e-3, (drift, dbpp)

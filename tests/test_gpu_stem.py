@@ -135,3 +135,25 @@ def test_stem_full_size_matches_direct(dev, case):
     scale = float(yd.abs().max())
     diff = float((ys - yd).abs().max()) / scale
     assert diff <= 1e-6, diff
+
+
+@pytest.mark.parametrize("cin", [2, 3, 6])
+def test_stem_pad_channels_masked(dev, cin):
+    """the pad channels (cin .. pitch-1) are masked at staging, so garbage a producer left
+    there (NaN, Inf, huge values) changes nothing: the output equals the zero-padded input's, bit for
+    bit, and the overflow flag stays clear."""
+    g = torch.Generator().manual_seed(40 + cin)
+    cout, k, s = (128, 3, 2) if cin == 2 else ((64, 5, 2) if cin == 3 else (64, 3, 1))
+    w = torch.randn(cout, cin, k, k, generator=g) * (1.0 / (cin * k * k) ** 0.5)
+    ps, _ = _packs(dev, w, torch.zeros(cout), s)
+    x = torch.rand(2, 24, 70, K.cp4(cin), generator=g)
+    x[..., cin:] = 0.0
+    xg = x.clone()
+    pads = K.cp4(cin) - cin
+    fill = torch.tensor([float("nan"), float("inf"), -1e30, 7.0])
+    xg[..., cin:] = fill[torch.arange(pads) % 4]
+    K.x3_overflow(reset=True)
+    y0, y1 = ps(x.to(dev)), ps(xg.to(dev))
+    torch.cuda.synchronize()
+    assert not K.x3_overflow(reset=True)
+    assert torch.equal(y0, y1)
