@@ -59,3 +59,56 @@ def test_pipeline_equals_serialised_launches(dev):
                           timeout=240)
     assert conc.returncode == 0, conc.stderr[-3000:]
     assert _digest(ser.stdout) == _digest(conc.stdout)
+
+
+# Production conv families at 4K as antagonists of the warp gathers (profiles/r6/race/README.md: on
+# gfx950 a kernel issuing dense MFMA chains beside a gather kernel can make lanes 48-63 of gathered
+# loads return zeros; the 7x7 stem experiment does, none of these may)
+_ANTAGONISTS = [
+    # (cin, cout, k, stride, transposed, level shift, in_op, act)
+    (8, 32, 7, 1, False, 0, "IN_NONE", "ACT_RELU"),      # SpyNet conv1 (direct x3)
+    (32, 64, 7, 1, False, 0, "IN_NONE", "ACT_RELU"),     # SpyNet conv2 (wr7)
+    (64, 64, 3, 1, False, 0, "IN_RELU", "ACT_RELU"),     # Warp_net ResBlock (Winograd)
+    (128, 128, 3, 2, True, 1, "IN_NONE", "ACT_LRELU"),   # mvDecoder deconv (dx)
+    (128, 128, 3, 2, False, 1, "IN_NONE", "ACT_LRELU"),  # mvEncoder conv (x3, stride 2)
+    (6, 64, 3, 1, False, 0, "IN_NONE", "ACT_RELU"),      # Warp_net feature_ext (stem)
+    (16, 2, 7, 1, False, 0, "IN_NONE", "ACT_NONE"),      # SpyNet conv5 (fp32 kernel)
+]
+
+
+@pytest.mark.timeout(300)
+def test_production_convs_leave_warp_gathers_exact(dev):
+    """Each production conv family runs back to back on one stream while the motion-compensation
+    warp (fvc_mc_assemble, data-dependent 4-tap gathers) runs on another at 4K: every warp output
+    equals the one made with the conv stream idle (on-device compare, no host sync per launch)."""
+    from fastvideocodec_amd import kernels as K
+    H, W = 2176, 3840
+    g = torch.Generator().manual_seed(3)
+    ref = torch.rand(1, H, W, 4, generator=g)
+    ref[..., 3] = 0
+    mv = (torch.rand(1, H, W, 4, generator=g) - 0.5) * 6
+    mv[..., 2:] = 0
+    ref, mv = ref.to(dev), mv.to(dev)
+    sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
+    with torch.cuda.stream(sb):
+        gold, _ = K.mc_assemble(ref, mv)
+    torch.cuda.synchronize()
+    bad = {}
+    for cin, cout, k, s, tr, sh, iop, act in _ANTAGONISTS:
+        wt = torch.randn((cin, cout, k, k) if tr else (cout, cin, k, k), generator=g) * (1.0 / (cin * k * k) ** 0.5)
+        p = K.PackedConv(wt, torch.zeros(cout), k, s, tr, dev, precision="x3")
+        x = torch.rand(1, H >> sh, W >> sh, K.cp4(cin), device=dev)
+        x[..., cin:] = 0
+        n = torch.zeros((), dtype=torch.int64, device=dev)
+        torch.cuda.synchronize()
+        for _ in range(16):
+            with torch.cuda.stream(sa):
+                for _ in range(2):
+                    p(x, in_op=getattr(K, iop), act=getattr(K, act))
+            with torch.cuda.stream(sb):
+                for _ in range(4):
+                    wf, _ = K.mc_assemble(ref, mv)
+                    n += (wf != gold).any(-1).sum()
+        torch.cuda.synchronize()
+        bad[f"{cin}->{cout} k{k} s{s}{' T' if tr else ''}"] = int(n)
+    assert all(v == 0 for v in bad.values()), bad
