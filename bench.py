@@ -704,7 +704,9 @@ def roofline_fields(prof, job, args):
                      "achieved_is": "algorithmic fp32-conv FLOP (2 x MAC of the direct convolution) / kernel time; "
                                     "the direct kernel issues 3 f16 MFMAs per MAC (ceiling peak/3), the Winograd "
                                     "kernel 3 per 16/36 MAC (ceiling peak/3 x 36/16), the Winograd-rows kernel 3 per "
-                                    "28/49 MAC (ceiling peak/3 x 49/28)",
+                                    "28/49 MAC (ceiling peak/3 x 49/28); frac_issued / issued_tflops count the f16 "
+                                    "MFMA FLOP each family issues per algorithmic FLOP as measured by SQ_INSTS_MFMA "
+                                    "(bench.ISSUED_PER_FLOP, profiles/r6/pmc_families.txt: padding included)",
                      "x3_ceiling": round(F16_MFMA_PEAK_TFLOPS / 3, 1),
                      "frac_of_x3_ceiling": round(achieved / (F16_MFMA_PEAK_TFLOPS / 3), 4),
                      **issued_fields(prof, x3_ms),
@@ -727,7 +729,12 @@ def roofline_fields(prof, job, args):
 # f16 MFMA FLOP issued per algorithmic fp32-conv FLOP, per kernel family: 3 split products (hi*hi,
 # hi*lo, lo*hi) per MAC; Winograd F(2x2,3x3) computes 16 products per 36 direct MACs, the
 # Winograd-rows F(2,7) 28 per 49
-ISSUED_PER_FLOP = {"x3": 3.0, "dx": 3.0, "wino": 3.0 * 16.0 / 36.0, "wr7": 3.0 * 28.0 / 49.0, "stem": 3.0}
+# f16 MFMA FLOP issued per algorithmic FLOP, per family: SQ_INSTS_MFMA x FLOP per instruction over
+# the bench's serial pass / the pass's algorithmic FLOP (profiles/r6/pmc_families.txt, r6). The
+# models they replace (direct 3, Winograd 3 x 16/36, Winograd-rows 3 x 28/49) miss the K padding
+# of the small-cin stems (3 -> 4.68: K rounded up to whole 16-deep k-steps), the x3 / dx tile
+# padding (3.16 / 3.10) and the tap-partial epilogues' MFMAs (Winograd 1.348)
+ISSUED_PER_FLOP = {"x3": 3.156, "dx": 3.101, "wino": 1.348, "wr7": 1.716, "stem": 4.685}
 
 
 def issued_fields(prof, fam_ms):
@@ -773,7 +780,7 @@ def load_pmc_traffic(H, W, gops):
     over `bench.py --serial` (profiles/<round>/x3_traffic.json, written by scripts/rocprof_summary.py;
     FETCH_SIZE doubled per MI355X_MICROARCH.md's gfx950 correction). PMC passes serialise every
     dispatch and cannot run inside the timed region, so the figure is the profiled one."""
-    for rnd in ("r5", "r4", "r3", "r2", "r1"):
+    for rnd in ("r6", "r5", "r4", "r3", "r2", "r1"):
         path = os.path.join(REPO, "profiles", rnd, "x3_traffic.json")
         try:
             with open(path) as f:

@@ -85,8 +85,8 @@ def main():
     out["split_family"] = dict(tflop_issued=tot_flop / 1e12, ms=tot_ns / 1e6, tflops_issued=fam_tf, frac_issued=fam_tf / 2500)
     if a.bench_json:
         b = json.load(open(a.bench_json))["roofline"]
-        lines.append(f"bench.py (HIP events, unprofiled): frac_issued {b.get('frac_issued')}, issued {b.get('issued_tflops')} "
-                     f"TF/s; algorithmic frac {b['frac']} ({b['achieved']} TF/s)")
+        lines.append(f"bench line of {os.path.basename(a.bench_json)} (HIP events): frac_issued {b.get('frac_issued')}, "
+                     f"issued {b.get('issued_tflops')} TF/s; algorithmic frac {b['frac']} ({b['achieved']} TF/s)")
     txt = "\n".join(lines)
     print(txt)
     if a.out:
