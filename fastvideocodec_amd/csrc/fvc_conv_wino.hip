@@ -70,7 +70,8 @@ constexpr int kChunk = 16;         // items per schedule chunk (consecutive tile
 constexpr float kLoScale = 2048.f;
 // knock-outs (experiment builds only; results wrong): FVC_WINO_KO bit 1 = no k-step-1 MFMAs,
 // 2 = no k-step-0 MFMAs (their split VALU kept), 4 = no item barrier, 8 = no finishing pass,
-// 16 = finishing pass without its output stores, 32 = finishing pass without its Z reads
+// 16 = finishing pass without its output stores, 32 = finishing pass without its Z reads,
+// 64 = no staging of the next item's input rows (LDS-DMA issue and its scalar addressing)
 #ifndef FVC_WINO_KO
 #define FVC_WINO_KO 0
 #endif
@@ -379,6 +380,7 @@ __global__ __launch_bounds__(256, 1) void conv_wino_kernel(const WinoArgs a) {
       // the next item's new input rows (2, or 4 after a chunk change), issued between the MFMA
       // blocks of the k-loop (k-th pair of rows at point k) where their issue cost overlaps them
       auto stage_next = [&](int k) {
+        if constexpr (FVC_WINO_KO & 64) return;  // knock-out: no staging of the next item's rows
         if (!nvalid) return;
         if (k == 0 && cont) return;
         const int i0 = 2 * k;
