@@ -44,6 +44,7 @@ _SIGS = {
     "fvc_conv_wino_wpack_bytes": (c_size_t, []),
     "fvc_conv_wino_pack_weight": (c_int, [vp, vp, vp]),
     "fvc_conv2d_nhwc_wino": (c_int, [vp, vp, c_float, vp, vp, vp, vp] + [c_int] * 6 + [vp, vp, c_int, vp]),
+    "fvc_conv2d_nhwc_wino_up": (c_int, [vp, vp, vp, vp, c_float, vp, vp] + [c_int] * 6 + [vp, vp, c_int, vp]),
     "fvc_conv_wino128_supported": (c_int, [c_int] * 5),
     "fvc_conv_wino128_wpack_bytes": (c_size_t, []),
     "fvc_conv_wino128_pack_weight": (c_int, [vp, vp, vp]),

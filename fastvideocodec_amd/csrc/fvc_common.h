@@ -45,3 +45,43 @@ __device__ __forceinline__ float4 fvc_apply_in_op4(float4 v, int op) {
   v.w = fvc_apply_in_op(v.w, op);
   return v;
 }
+
+// ------------------------------------------------------------------ bilinear upsampling (shared)
+// ATen compute_indices_weights_linear for align_corners=True with the scale (in-1)/(out-1)
+// precomputed (the caller computes it the same way: one correctly rounded float division), and the
+// bilinear combination in ATen's order (a l0x + b l1x) l0y + (c l0x + d l1x) l1y with explicit
+// fmaf, so the standalone upsample-add kernel (fvc_elem.hip) and the Winograd kernel's fused
+// upsample-add staging (fvc_conv_wino.hip) round identically.
+struct FvcUpIdx {
+  int i0, i1;
+  float l0, l1;
+};
+
+__device__ __forceinline__ FvcUpIdx fvc_up_index_scaled(int d, int in, float scale) {
+  // no contraction: src is rounded before the floor and the subtraction in every caller (with
+  // contraction the compiler may form lam = fma(scale, d, -i0) in one kernel and not in another)
+#pragma clang fp contract(off)
+  const float src = scale * (float)d;
+  int i0 = (int)floorf(src);
+  const float lam = fminf(fmaxf(src - (float)i0, 0.f), 1.f);
+  if (i0 > in - 1) i0 = in - 1;
+  FvcUpIdx u;
+  u.i0 = i0;
+  u.i1 = i0 + ((i0 < in - 1) ? 1 : 0);
+  u.l1 = lam;
+  u.l0 = 1.f - lam;
+  return u;
+}
+
+__device__ __forceinline__ float fvc_lerp2d(float a, float b, float c, float d, float l0x, float l1x, float l0y,
+                                            float l1y) {
+  return fmaf(fmaf(d, l1x, c * l0x), l1y, fmaf(b, l1x, a * l0x) * l0y);
+}
+
+__device__ __forceinline__ float4 fvc_lerp2d4(const float4& a, const float4& b, const float4& c, const float4& d,
+                                              const FvcUpIdx& uy, const FvcUpIdx& ux) {
+  return make_float4(fvc_lerp2d(a.x, b.x, c.x, d.x, ux.l0, ux.l1, uy.l0, uy.l1),
+                     fvc_lerp2d(a.y, b.y, c.y, d.y, ux.l0, ux.l1, uy.l0, uy.l1),
+                     fvc_lerp2d(a.z, b.z, c.z, d.z, ux.l0, ux.l1, uy.l0, uy.l1),
+                     fvc_lerp2d(a.w, b.w, c.w, d.w, ux.l0, ux.l1, uy.l0, uy.l1));
+}

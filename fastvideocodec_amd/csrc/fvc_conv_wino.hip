@@ -66,6 +66,14 @@ constexpr int kRingBytes = kRing * kRowEntries * 16;  // 81920
 constexpr int kZBytes = 4 * 8 * 1024;                 // one Z buffer: 4 waves x 8 planes x 1 KB
 constexpr int kHdr = 512;                             // bias (256 B) + schedule words
 constexpr int kLds = kHdr + kRingBytes + 2 * kZBytes; // 148,480 B
+// fused upsample-add input (UP): the low-resolution rows one item's fix-up reads, [row][pixel][quad]
+// (up to 4 source rows x 20 source columns, the span 4 output rows x 34 output columns of a 2x
+// align_corners=True upsample can reach); Z single-buffered (two barriers per item)
+constexpr int kLowRows = 4;
+constexpr int kLowCols = 20;
+constexpr int kLowRowEnt = kLowCols * kQ;                  // 16-B entries per low row (320)
+constexpr int kLowBytes = kLowRows * kLowRowEnt * 16;      // 20,480
+constexpr int kLdsUp = kHdr + kRingBytes + kZBytes + kLowBytes;  // 135,680 B
 constexpr int kChunk = 16;         // items per schedule chunk (consecutive tile rows of one column)
 constexpr float kLoScale = 2048.f;
 // knock-outs (experiment builds only; results wrong): FVC_WINO_KO bit 1 = no k-step-1 MFMAs,
@@ -74,6 +82,15 @@ constexpr float kLoScale = 2048.f;
 // 64 = no staging of the next item's input rows (LDS-DMA issue and its scalar addressing)
 #ifndef FVC_WINO_KO
 #define FVC_WINO_KO 0
+#endif
+// UP knock-outs / forms (experiment builds only): FVC_UP_KO bit 1 = no fix-up body, 2 = no second
+// barrier, 4 = no xu stores, 8 = no LDS write-back, 16 = no low-row DMA; FVC_UP_FORM 1 = per-entry
+// lerp (four low taps per entry) instead of the shared horizontal lerps
+#ifndef FVC_UP_KO
+#define FVC_UP_KO 0
+#endif
+#ifndef FVC_UP_FORM
+#define FVC_UP_FORM 0
 #endif
 #ifndef FVC_WINO_KO_WAIT
 #define FVC_WINO_KO_WAIT 0
@@ -111,9 +128,19 @@ struct WinoArgs {
   // pixel pitch (floats) of x and of y / res: 64, or 128 for a quarter of a 128 -> 128 conv
   // (x, y, res then point at the first channel of their 64-channel half)
   int xp, yp;
+  // UP: x is the skip tensor S (full resolution, pitch 64); the input the conv reads is
+  // X = S + up2(L) (bilinear, align_corners=True, L = xl [B][hl][wl][64], H = 2 hl, W = 2 wl), formed
+  // in LDS after each row's LDS-DMA and written to xu (every pixel once) for the caller's residual
+  const float* xl;
+  float* xu;
+  int hl, wl;
+  float usy, usx;  // (hl - 1) / (H - 1), (wl - 1) / (W - 1), one correctly rounded float division each
 };
 
 typedef __attribute__((address_space(3))) void* lds_ptr;
+
+// UP: quad swizzle of the low rows' LDS image (pixel p's quad q at slot q ^ low_swz(p))
+__device__ __forceinline__ int low_swz(int p) { return (p & 3) << 2; }
 
 // a raw buffer descriptor over [p, p + bytes): offsets at or past `bytes` read 0 / drop the store.
 // The inputs go through readfirstlane (free on values already in SGPRs): the compiler must see the
@@ -223,13 +250,15 @@ __device__ __forceinline__ void split2(float v0, float v1, unsigned& hi, unsigne
 
 // RES: 0 none, kResPost = y = act(conv + bias) + res (ResBlock), kResPre = y = act(conv + bias + res)
 // (the second input half of a 128 -> 128 conv adding the first half's partial sum)
-template <int IOP, int POST, int RES, int ACT>
+template <int IOP, int POST, int RES, int ACT, bool UP = false>
 __global__ __launch_bounds__(256, 1) void conv_wino_kernel(const WinoArgs a) {
+  static_assert(!UP || (POST == 0 && RES == 0), "the fused upsample-add input is a plain-conv form");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* const sbias = reinterpret_cast<float*>(smem);
   int* const sq = reinterpret_cast<int*>(smem + 256);  // [0..1] first chunks, [2..3] chunk after next
   char* const ring = smem + kHdr;
   char* const zbuf = ring + kRingBytes;
+  char* const low = zbuf + (UP ? 1 : 2) * kZBytes;  // UP: the low-resolution rows of the next fix-up
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -319,6 +348,214 @@ __global__ __launch_bounds__(256, 1) void conv_wino_kernel(const WinoArgs a) {
     }
     return p;
   };
+  // ---- UP: the fix-up X = S + up2(L) of the rows an item adds to the ring. The rows land by
+  // LDS-DMA as S; the low-resolution rows they need land in `low` by LDS-DMA as well (issued with the
+  // rows, during the previous item's k-loop); after the item barrier every thread rewrites its
+  // entries in place (ring entry = S + lerp of four low taps, the same arithmetic as the standalone
+  // k_up2_add_q16p), writes the ones its chunk owns to xu, and a second barrier publishes them.
+  struct Fix {
+    int b, g, r0, nr, sbase;  // output rows [r0, r0 + nr) of column group g of image b, at ring slot sbase..
+    int own0, own1;           // rows [own0, own1) are this chunk's to write to xu
+    int lr0, nlow, lc0, ncol; // low rows / columns staged in `low` (nlow = 0: nothing to do)
+  };
+  auto make_fix = [&](const Pos& p, int ty, bool contd, int sb) -> Fix {
+    Fix f;
+    f.b = p.b;
+    f.g = p.g;
+    f.r0 = contd ? 2 * ty + 1 : 2 * ty - 1;
+    f.nr = contd ? 2 : 4;
+    f.sbase = contd ? (sb + 2) & (kRing - 1) : sb;
+    f.own0 = 2 * p.ty0;
+    f.own1 = 2 * p.ty1;
+    const int rf = max(f.r0, 0), rl = min(f.r0 + f.nr - 1, H - 1);
+    const int cf = max(32 * p.g - 1, 0), cl = min(32 * p.g + 32, W - 1);
+    f.lr0 = fvc_up_index_scaled(rf, a.hl, a.usy).i0;
+    f.nlow = rf <= rl ? fvc_up_index_scaled(rl, a.hl, a.usy).i1 - f.lr0 + 1 : 0;
+    f.lc0 = fvc_up_index_scaled(cf, a.wl, a.usx).i0;
+    f.ncol = fvc_up_index_scaled(cl, a.wl, a.usx).i1 - f.lc0 + 1;
+    f.lr0 = __builtin_amdgcn_readfirstlane(f.lr0);
+    f.nlow = __builtin_amdgcn_readfirstlane(f.nlow);
+    f.lc0 = __builtin_amdgcn_readfirstlane(f.lc0);
+    f.ncol = __builtin_amdgcn_readfirstlane(f.ncol);
+    return f;
+  };
+  // the low rows of fix-up f into `low`: 4 rows x 5 pieces of 64 x 16 B (4 pixels each), piece
+  // wave + 4 m of this wave; bytes past the row's ncol pixels read as zeros (never used). Entry
+  // (pixel p, quad q) sits at p * 16 + (q ^ low_swz(p)): the fix-up's lanes read 16 pixels x 4 quads
+  // at once, which unswizzled (256-B pixel pitch = all 64 banks) would hit the same 4 banks 16 times
+  // over; the swizzle is applied on the global side (each lane's 16-B source), so the LDS-DMA image
+  // stays lane-linear and every piece still reads 1 KB of consecutive bytes
+  auto stage_low = [&](const Fix& f) {
+    if constexpr ((FVC_UP_KO & 16) != 0) return;
+    const int e = lane >> 4, qq = lane & 15;  // pixel within the piece, LDS quad slot
+#pragma unroll
+    for (int m = 0; m < 5; ++m) {
+      const int pc = wave + 4 * m, row = pc / 5, pr = pc - 5 * row;
+      if (row < f.nlow) {
+        const __amdgpu_buffer_rsrc_t rl =
+            rsrc(a.xl + ((size_t)((unsigned)f.b * a.hl + f.lr0 + row) * a.wl + f.lc0) * kC, (unsigned)f.ncol * kC * 4u);
+        const int px = 4 * pr + e;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rl, (lds_ptr)(low + ((size_t)row * kLowRowEnt + pr * 64) * 16), 16,
+                                                 (unsigned)(px * kQ + (qq ^ low_swz(px))) * 16u, 0, 0, 0);
+      }
+    }
+  };
+  auto fixup_entry = [&](const Fix& f) {  // FVC_UP_FORM 1
+    if (f.nlow <= 0) return;
+    for (int cmb = tid; cmb < 4 * 34 * 4; cmb += 256) {
+      const int qlo = cmb & 3, rest = cmb >> 2;
+      const int qhi = rest / 34, sl = rest - 34 * qhi;
+      const int q = 4 * qhi + qlo;
+      const int c = sl < 17 ? 2 * sl : 2 * (sl - 17) + 1;
+      const int ox = 32 * f.g - 1 + c;
+      if ((unsigned)ox >= (unsigned)W) continue;
+      const FvcUpIdx ux = fvc_up_index_scaled(ox, a.wl, a.usx);
+      const int pa = ux.i0 - f.lc0, pb = ux.i1 - f.lc0;
+      const int xa = pa * kQ + (q ^ low_swz(pa)), xb = pb * kQ + (q ^ low_swz(pb));
+      const bool own_c = c >= 1 && c <= 32;
+      for (int ri = 0; ri < f.nr; ++ri) {
+        const int r = f.r0 + ri;
+        if ((unsigned)r >= (unsigned)H) continue;
+        const FvcUpIdx uy = fvc_up_index_scaled(r, a.hl, a.usy);
+        const int ya = (uy.i0 - f.lr0) * kLowRowEnt, yb = (uy.i1 - f.lr0) * kLowRowEnt;
+        float4* const pe =
+            reinterpret_cast<float4*>(ring + ((size_t)((f.sbase + ri) & (kRing - 1)) * kRowEntries + q * kSlots + sl) * 16);
+        const float4* const lw = reinterpret_cast<const float4*>(low);
+        const float4 sk = *pe;
+        const float4 v = fvc_lerp2d4(lw[ya + xa], lw[ya + xb], lw[yb + xa], lw[yb + xb], uy, ux);
+        const float4 xs = make_float4(sk.x + v.x, sk.y + v.y, sk.z + v.z, sk.w + v.w);
+        if constexpr (!(FVC_UP_KO & 8)) *pe = xs;
+        if constexpr (!(FVC_UP_KO & 4)) {
+          if (own_c && r >= f.own0 && r < f.own1)
+            *reinterpret_cast<float4*>(a.xu + (((size_t)f.b * H + r) * W + ox) * kC + 4 * q) = xs;
+        } else {
+          asm volatile("" ::"v"(xs.x), "v"(xs.y), "v"(xs.z), "v"(xs.w));
+        }
+      }
+    }
+  };
+  // rows ri0, ri0 + 1 of fix-up f, all of this thread's entries at once: every LDS read (the entries
+  // and the low taps) is issued before the first result is formed, so the reads' latency is paid
+  // once per pair of rows instead of once per entry. A fix-up's row pairs (2m + 1, 2m + 2) of a 2x
+  // align_corners upsample share their two low rows (both floor to m); then (SHARED) each low row's
+  // horizontal lerp fmaf(b, l1x, a * l0x) is formed once for both rows: 4 low taps per column
+  // instead of 8. Invalid entries (past the 544 (column slot, quad) pairs, outside the image) read
+  // a safe address and write nothing.
+  auto fixup_rows = [&](const Fix& f, int ri0) {
+    bool rv[2], ro[2];
+    int ya[2], yb[2];
+    float ly0[2], ly1[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int ri = ri0 + k, r = f.r0 + ri;
+      rv[k] = ri < f.nr && (unsigned)r < (unsigned)H;
+      ro[k] = rv[k] && r >= f.own0 && r < f.own1;
+      const FvcUpIdx uy = fvc_up_index_scaled(rv[k] ? r : max(f.r0, 0), a.hl, a.usy);
+      ya[k] = __builtin_amdgcn_readfirstlane((uy.i0 - f.lr0) * kLowRowEnt);
+      yb[k] = __builtin_amdgcn_readfirstlane((uy.i1 - f.lr0) * kLowRowEnt);
+      ly0[k] = uy.l0;
+      ly1[k] = uy.l1;
+    }
+    if (!rv[0] && !rv[1]) return;
+    // the pair's xu rows (32-bit lane offsets; bytes past the image drop)
+    const int rxf = f.r0 + ri0 + (rv[0] ? 0 : 1);
+    const __amdgpu_buffer_rsrc_t rxu = rsrc(a.xu + ((size_t)f.b * H + rxf) * W * kC, (unsigned)(min(H - rxf, 2) * W) * kC * 4u);
+    const float4* const lw = reinterpret_cast<const float4*>(low);
+    const bool shared = rv[0] && rv[1] && ya[0] == ya[1] && yb[0] == yb[1];  // wave-uniform
+    unsigned lo[3], xo[3];
+    bool ok[3], own[3];
+    FvcUpIdx ux[3];
+    int xa[3], xb[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const int cmb0 = tid + 256 * j;
+      ok[j] = cmb0 < 4 * 34 * 4;
+      const int cmb = ok[j] ? cmb0 : tid;
+      const int qlo = cmb & 3, rest = cmb >> 2;
+      const int qhi = rest / 34, sl = rest - 34 * qhi;
+      const int q = 4 * qhi + qlo;
+      const int c = sl < 17 ? 2 * sl : 2 * (sl - 17) + 1;
+      const int ox = 32 * f.g - 1 + c;
+      ok[j] = ok[j] && (unsigned)ox < (unsigned)W;
+      own[j] = c >= 1 && c <= 32;
+      const int oxc = min(max(ox, 0), W - 1);
+      ux[j] = fvc_up_index_scaled(oxc, a.wl, a.usx);
+      const int pa = ux[j].i0 - f.lc0, pb = ux[j].i1 - f.lc0;
+      xa[j] = pa * kQ + (q ^ low_swz(pa));
+      xb[j] = pb * kQ + (q ^ low_swz(pb));
+      lo[j] = (unsigned)(q * kSlots + sl) * 16u;
+      xo[j] = (unsigned)(oxc * kC + 4 * q) * 4u;
+    }
+    char* const rw0 = ring + (size_t)((f.sbase + ri0) & (kRing - 1)) * kRowEntries * 16;
+    char* const rw1 = ring + (size_t)((f.sbase + ri0 + 1) & (kRing - 1)) * kRowEntries * 16;
+    auto put = [&](int j, int k, const float4& sk, const float4& v) {
+      const float4 xs = make_float4(sk.x + v.x, sk.y + v.y, sk.z + v.z, sk.w + v.w);
+      if (ok[j] && rv[k]) {
+        if constexpr (!(FVC_UP_KO & 8)) *reinterpret_cast<float4*>((k ? rw1 : rw0) + lo[j]) = xs;
+        if constexpr (!(FVC_UP_KO & 4)) {
+          if (own[j] && ro[k])
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, xs), rxu,
+                                                   (unsigned)(f.r0 + ri0 + k - rxf) * (unsigned)W * kC * 4u + xo[j], 0, 0);
+        } else {
+          asm volatile("" ::"v"(xs.x), "v"(xs.y), "v"(xs.z), "v"(xs.w));
+        }
+      }
+    };
+    auto hlerp = [&](const float4& ta, const float4& tb, const FvcUpIdx& u) {
+      return make_float4(fmaf(tb.x, u.l1, ta.x * u.l0), fmaf(tb.y, u.l1, ta.y * u.l0), fmaf(tb.z, u.l1, ta.z * u.l0),
+                         fmaf(tb.w, u.l1, ta.w * u.l0));
+    };
+    auto vlerp = [&](const float4& h0, const float4& h1, int k) {  // = fvc_lerp2d's outer step
+      return make_float4(fmaf(h1.x, ly1[k], h0.x * ly0[k]), fmaf(h1.y, ly1[k], h0.y * ly0[k]),
+                         fmaf(h1.z, ly1[k], h0.z * ly0[k]), fmaf(h1.w, ly1[k], h0.w * ly0[k]));
+    };
+    if (shared) {
+      float4 t[3][6];  // two entries, then the four taps
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        t[j][0] = *reinterpret_cast<const float4*>(rw0 + lo[j]);
+        t[j][1] = *reinterpret_cast<const float4*>(rw1 + lo[j]);
+        t[j][2] = lw[ya[0] + xa[j]];
+        t[j][3] = lw[ya[0] + xb[j]];
+        t[j][4] = lw[yb[0] + xa[j]];
+        t[j][5] = lw[yb[0] + xb[j]];
+      }
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        const float4 h0 = hlerp(t[j][2], t[j][3], ux[j]), h1 = hlerp(t[j][4], t[j][5], ux[j]);
+        put(j, 0, t[j][0], vlerp(h0, h1, 0));
+        put(j, 1, t[j][1], vlerp(h0, h1, 1));
+      }
+    } else {
+      float4 t[3][2][5];
+#pragma unroll
+      for (int j = 0; j < 3; ++j)
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          t[j][k][0] = *reinterpret_cast<const float4*>((k ? rw1 : rw0) + lo[j]);
+          t[j][k][1] = lw[ya[k] + xa[j]];
+          t[j][k][2] = lw[ya[k] + xb[j]];
+          t[j][k][3] = lw[yb[k] + xa[j]];
+          t[j][k][4] = lw[yb[k] + xb[j]];
+        }
+#pragma unroll
+      for (int j = 0; j < 3; ++j)
+#pragma unroll
+        for (int k = 0; k < 2; ++k)
+          put(j, k, t[j][k][0], vlerp(hlerp(t[j][k][1], t[j][k][2], ux[j]), hlerp(t[j][k][3], t[j][k][4], ux[j]), k));
+    }
+  };
+  auto fixup = [&](const Fix& f) {
+    if constexpr ((FVC_UP_KO & 1) != 0) return;
+    if (f.nlow <= 0) return;
+    if constexpr (FVC_UP_FORM == 1) {
+      fixup_entry(f);
+      return;
+    }
+    fixup_rows(f, 0);
+    if (f.nr > 2) fixup_rows(f, 2);
+  };
+
   // the block knows its current and next chunk; the first item of every chunk takes the one
   // after (thread 0, into LDS word 2 + parity, decoded by everyone after that item's barrier)
   if (tid == 0) {
@@ -365,8 +602,17 @@ __global__ __launch_bounds__(256, 1) void conv_wino_kernel(const WinoArgs a) {
     row_offsets(cur.g, vo_cur);
     out_offsets(cur.g);
     for (int i = 0; i < 4; ++i) stage_row(xi_cur, 2 * cur.ty0 - 1 + i, i, vo_cur);
+    Fix f0 = {};
+    if constexpr (UP) {
+      f0 = make_fix(cur, cur.ty0, false, 0);
+      stage_low(f0);
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    if constexpr (UP) {
+      fixup(f0);
+      __syncthreads();
+    }
     int ty = cur.ty0;
     int base = 0;  // ring slot of the current item's first row
     int zb = 0;    // Z buffer
@@ -377,6 +623,10 @@ __global__ __launch_bounds__(256, 1) void conv_wino_kernel(const WinoArgs a) {
       const int nty = cont ? ty + 1 : nxt.ty0;
       const bool nvalid = cont || nxt.ty0 < nxt.ty1;
       const int nbase = (base + (cont ? 2 : 4)) & (kRing - 1);
+      Fix nf = {};  // UP: the fix-up of the next item's new rows (nothing when there is no next item)
+      if constexpr (UP) {
+        if (nvalid) nf = make_fix(np, nty, cont, nbase);
+      }
       // the next item's new input rows (2, or 4 after a chunk change), issued between the MFMA
       // blocks of the k-loop (k-th pair of rows at point k) where their issue cost overlaps them
       auto stage_next = [&](int k) {
@@ -391,6 +641,9 @@ __global__ __launch_bounds__(256, 1) void conv_wino_kernel(const WinoArgs a) {
           row_offsets(np.g, vo);
           const float* xi_np = a.x + (size_t)np.b * ximg_e;
           for (int i = i0; i < i0 + 2; ++i) stage_row(xi_np, 2 * nty - 1 + i, (nbase + i) & (kRing - 1), vo);
+        }
+        if constexpr (UP) {
+          if (k == 1) stage_low(nf);
         }
       };
       if (first && tid == 0) sq[2 + (ntaken & 1)] = take(ntaken);  // chunk after next
@@ -658,6 +911,11 @@ __global__ __launch_bounds__(256, 1) void conv_wino_kernel(const WinoArgs a) {
 
       }  // FVC_WINO_KO & 8
 
+      if constexpr (UP) {  // the next item's new rows: S -> X in place (and to xu), then published
+        fixup(nf);
+        if constexpr (!(FVC_UP_KO & 2)) __syncthreads();
+      }
+
       // ---- advance
       if (!nvalid) break;
       if (!cont) {
@@ -672,7 +930,7 @@ __global__ __launch_bounds__(256, 1) void conv_wino_kernel(const WinoArgs a) {
       }
       ty = nty;
       base = nbase;
-      zb ^= 1;
+      if constexpr (!UP) zb ^= 1;
     }
   }
   {
@@ -704,14 +962,23 @@ static int env_int(const char* n, int dflt) {
   return (v && v[0]) ? atoi(v) : dflt;
 }
 
-template <int IOP, int POST, int RES, int ACT>
+template <int IOP, int POST, int RES, int ACT, bool UP = false>
 static int wino_launch4(const WinoArgs& a, int grid, hipStream_t s) {
-  const hipError_t e = hipFuncSetAttribute((const void*)conv_wino_kernel<IOP, POST, RES, ACT>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, kLds);
+  const int lds = UP ? kLdsUp : kLds;
+  const hipError_t e = hipFuncSetAttribute((const void*)conv_wino_kernel<IOP, POST, RES, ACT, UP>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, lds);
   if (e != hipSuccess) return -(int)e;
-  hipLaunchKernelGGL((conv_wino_kernel<IOP, POST, RES, ACT>), dim3(grid), dim3(256), kLds, s, a);
+  hipLaunchKernelGGL((conv_wino_kernel<IOP, POST, RES, ACT, UP>), dim3(grid), dim3(256), lds, s, a);
   FVC_CHECK_LAUNCH();
   return 0;
+}
+
+// the fused upsample-add input form: plain conv (no residual, no pool / tap epilogue)
+template <int IOP>
+static int wino_launch_up(const WinoArgs& a, int act, hipStream_t s, int grid) {
+  if (act == FVC_ACT_NONE) return wino_launch4<IOP, 0, 0, FVC_ACT_NONE, true>(a, grid, s);
+  if (act == FVC_ACT_RELU) return wino_launch4<IOP, 0, 0, FVC_ACT_RELU, true>(a, grid, s);
+  return wino_launch4<IOP, 0, 0, FVC_ACT_LRELU, true>(a, grid, s);
 }
 
 // instantiated: Warp_net's forms (ResBlock conv1: ReLU in, ReLU act; conv2: residual, with or
@@ -743,8 +1010,11 @@ static int wino_launch_pre(const WinoArgs& a, int act, hipStream_t s, int grid) 
 static int run_wino(const float* x, const void* upack, float osc, const float* bias, const float* res, float* y,
                     float* pool, int batch, int h, int w, int in_op, int act, int cu_reserve, int* ovf, int* sched,
                     int sched_len, hipStream_t s, const void* tw = nullptr, float tosc = 0.f, int pcp = 0,
-                    int pitch = kC, bool res_pre = false) {
+                    int pitch = kC, bool res_pre = false, const float* xl = nullptr, float* xu = nullptr) {
   if (tw && (pool || in_op != FVC_IN_NONE || pcp <= 0 || pcp > 32 || (pcp & 3))) return FVC_EINVAL;
+  // UP: x is the skip S, xl the half-resolution source, xu receives S + up2(xl)
+  if ((xl != nullptr) != (xu != nullptr)) return FVC_EINVAL;
+  if (xl && (tw || pool || res || pitch != kC || (h & 1) || (w & 1))) return FVC_EINVAL;
   if (!x || !upack || (!bias && pitch == kC) || !y || batch <= 0 || h <= 0 || w <= 0 || cu_reserve < 0 ||
       sched_len < 0)
     return FVC_EINVAL;
@@ -776,12 +1046,23 @@ static int run_wino(const float* x, const void* upack, float osc, const float* b
   a.tosc_c = tosc * (1.0f / 2048.f);
   a.pcp = pcp;
   a.xp = a.yp = pitch;
+  a.xl = xl;
+  a.xu = xu;
+  a.hl = h / 2;
+  a.wl = w / 2;
+  // ATen's align_corners=True scale (in - 1) / (out - 1), as k_up2_add_q16p computes it
+  a.usy = h > 1 ? (float)(a.hl - 1) / (float)(h - 1) : 0.f;
+  a.usx = w > 1 ? (float)(a.wl - 1) / (float)(w - 1) : 0.f;
   const int reserve = env_int("FVC_X3_RESERVE", -1) >= 0 ? env_int("FVC_X3_RESERVE", 0) : cu_reserve;
   const int ncu = wino_num_cus() - (reserve < wino_num_cus() / 2 ? reserve : wino_num_cus() / 2);
   int grid = ncu < a.nchunks ? ncu : a.nchunks;
   a.sched = (sched && sched_len >= 2 && env_int("FVC_X3_DYN", 1)) ? sched : nullptr;
   if (act != FVC_ACT_NONE && act != FVC_ACT_RELU && act != FVC_ACT_LRELU) return FVC_EINVAL;
   if (tw) return wino_launch<FVC_IN_NONE, kPostTap>(a, act, s, grid);
+  if (xl) {
+    if (in_op == FVC_IN_NONE) return wino_launch_up<FVC_IN_NONE>(a, act, s, grid);
+    return wino_launch_up<FVC_IN_RELU>(a, act, s, grid);
+  }
   if (res_pre) {
     if (in_op == FVC_IN_NONE) return wino_launch_pre<FVC_IN_NONE>(a, act, s, grid);
     return wino_launch_pre<FVC_IN_RELU>(a, act, s, grid);
@@ -947,6 +1228,17 @@ int fvc_conv2d_nhwc_wino128(const float* x, const void* wpack, const float* osc4
     if (r) return r;
   }
   return 0;
+}
+
+// y = conv(in_op(X)) with X = skip + up2(low) (bilinear, align_corners=True; Warp_net's
+// c3_u = c1 + up(c3) and c4_u = c0 + up(c4), endecoder.py:288-293) formed in the kernel's staging
+// and written to xsum (bit-identical to fvc_upsample2x_add_nhwc's output) for the consumer's residual
+int fvc_conv2d_nhwc_wino_up(const float* skip, const float* low, float* xsum, const void* wpack, float osc,
+                            const float* bias, float* y, int batch, int h, int w, int in_op, int act, int cu_reserve,
+                            int* overflow_flag, int* sched, int sched_len, fvc_stream_t stream) {
+  if (!skip || !low || !xsum) return FVC_EINVAL;
+  return run_wino(skip, wpack, osc, bias, nullptr, y, nullptr, batch, h, w, in_op, act, cu_reserve, overflow_flag,
+                  sched, sched_len, (hipStream_t)stream, nullptr, 0.f, 0, kC, false, low, xsum);
 }
 
 int fvc_conv2d_nhwc_wino(const float* x, const void* wpack, float osc, const float* bias, const float* res,

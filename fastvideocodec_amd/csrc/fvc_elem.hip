@@ -354,9 +354,10 @@ struct UpIdx {
 // ATen compute_indices_weights_linear: src = ac ? scale*d : max(scale*(d+0.5)-0.5, 0)
 __device__ __forceinline__ UpIdx up_index(int d, int in, int out, int ac) {
   float src;
-  if (ac) {
+  if (ac) {  // = fvc_up_index_scaled (fvc_common.h), which the Winograd kernel's fused staging uses
     const float scale = out > 1 ? (float)(in - 1) / (float)(out - 1) : 0.f;
-    src = scale * (float)d;
+    const FvcUpIdx f = fvc_up_index_scaled(d, in, scale);
+    return UpIdx{f.i0, f.i1, f.l0, f.l1};
   } else {
     const float scale = (float)in / (float)out;
     src = fmaxf(scale * ((float)d + 0.5f) - 0.5f, 0.f);
@@ -372,6 +373,17 @@ __device__ __forceinline__ UpIdx up_index(int d, int in, int out, int ac) {
   return u;
 }
 
+// the 2x upsample kernels' index: align_corners=True with the scale (in - 1) / (out - 1) computed once on
+// the host (the float division ATen performs on the CPU; the Winograd kernel's fused upsample-add
+// staging takes the same host value), else the half-pixel form of up_index
+__device__ __forceinline__ UpIdx up2_index(int d, int in, int out, int ac, float s) {
+  if (ac) {
+    const FvcUpIdx f = fvc_up_index_scaled(d, in, s);
+    return UpIdx{f.i0, f.i1, f.l0, f.l1};
+  }
+  return up_index(d, in, out, 0);
+}
+
 __device__ __forceinline__ float4 up_sample4(const float* src, size_t bbase, int w, int c4n, int c4,
                                              const UpIdx& uy, const UpIdx& ux) {
   const float4* s = reinterpret_cast<const float4*>(src);
@@ -380,10 +392,10 @@ __device__ __forceinline__ float4 up_sample4(const float* src, size_t bbase, int
   const float4 c = s[(bbase + (size_t)uy.i1 * w + ux.i0) * c4n + c4];
   const float4 d = s[(bbase + (size_t)uy.i1 * w + ux.i1) * c4n + c4];
   float4 o;
-  o.x = (a.x * ux.l0 + b.x * ux.l1) * uy.l0 + (c.x * ux.l0 + d.x * ux.l1) * uy.l1;
-  o.y = (a.y * ux.l0 + b.y * ux.l1) * uy.l0 + (c.y * ux.l0 + d.y * ux.l1) * uy.l1;
-  o.z = (a.z * ux.l0 + b.z * ux.l1) * uy.l0 + (c.z * ux.l0 + d.z * ux.l1) * uy.l1;
-  o.w = (a.w * ux.l0 + b.w * ux.l1) * uy.l0 + (c.w * ux.l0 + d.w * ux.l1) * uy.l1;
+  o.x = fvc_lerp2d(a.x, b.x, c.x, d.x, ux.l0, ux.l1, uy.l0, uy.l1);
+  o.y = fvc_lerp2d(a.y, b.y, c.y, d.y, ux.l0, ux.l1, uy.l0, uy.l1);
+  o.z = fvc_lerp2d(a.z, b.z, c.z, d.z, ux.l0, ux.l1, uy.l0, uy.l1);
+  o.w = fvc_lerp2d(a.w, b.w, c.w, d.w, ux.l0, ux.l1, uy.l0, uy.l1);
   return o;
 }
 
@@ -397,7 +409,7 @@ __device__ __forceinline__ unsigned udiv_magic(unsigned n, unsigned d, unsigned 
 }
 
 __global__ void k_up2_add_q16(const float* __restrict__ src, const float* __restrict__ skip, float* __restrict__ out,
-                              int B, int h, int w, int ac, float scale, unsigned mW, unsigned mH) {
+                              int B, int h, int w, int ac, float scale, unsigned mW, unsigned mH, float usy, float usx) {
   const unsigned H = 2u * h, W = 2u * w;
   const unsigned n = (unsigned)B * H * W * 16u;
   const float4* s4 = reinterpret_cast<const float4*>(src);
@@ -408,17 +420,17 @@ __global__ void k_up2_add_q16(const float* __restrict__ src, const float* __rest
     const int x = (int)(p - row * W);
     const unsigned b = udiv_magic(row, H, mH);
     const int y = (int)(row - b * H);
-    const UpIdx uy = up_index(y, h, (int)H, ac), ux = up_index(x, w, (int)W, ac);
+    const UpIdx uy = up2_index(y, h, (int)H, ac, usy), ux = up2_index(x, w, (int)W, ac, usx);
     const unsigned bb = b * (unsigned)h * (unsigned)w;
     const float4 a = s4[(bb + (unsigned)uy.i0 * w + ux.i0) * 16u + c4];
     const float4 bq = s4[(bb + (unsigned)uy.i0 * w + ux.i1) * 16u + c4];
     const float4 c = s4[(bb + (unsigned)uy.i1 * w + ux.i0) * 16u + c4];
     const float4 d = s4[(bb + (unsigned)uy.i1 * w + ux.i1) * 16u + c4];
     float4 v;
-    v.x = (a.x * ux.l0 + bq.x * ux.l1) * uy.l0 + (c.x * ux.l0 + d.x * ux.l1) * uy.l1;
-    v.y = (a.y * ux.l0 + bq.y * ux.l1) * uy.l0 + (c.y * ux.l0 + d.y * ux.l1) * uy.l1;
-    v.z = (a.z * ux.l0 + bq.z * ux.l1) * uy.l0 + (c.z * ux.l0 + d.z * ux.l1) * uy.l1;
-    v.w = (a.w * ux.l0 + bq.w * ux.l1) * uy.l0 + (c.w * ux.l0 + d.w * ux.l1) * uy.l1;
+    v.x = fvc_lerp2d(a.x, bq.x, c.x, d.x, ux.l0, ux.l1, uy.l0, uy.l1);
+    v.y = fvc_lerp2d(a.y, bq.y, c.y, d.y, ux.l0, ux.l1, uy.l0, uy.l1);
+    v.z = fvc_lerp2d(a.z, bq.z, c.z, d.z, ux.l0, ux.l1, uy.l0, uy.l1);
+    v.w = fvc_lerp2d(a.w, bq.w, c.w, d.w, ux.l0, ux.l1, uy.l0, uy.l1);
     if (scale != 1.f) { v.x *= scale; v.y *= scale; v.z *= scale; v.w *= scale; }
     if (skip) {
       const float4 sk = reinterpret_cast<const float4*>(skip)[e];
@@ -434,24 +446,24 @@ __global__ void k_up2_add_q16(const float* __restrict__ src, const float* __rest
 template <bool NT>
 __device__ __forceinline__ float4 up2_q16_elem(const float4* __restrict__ s4, const float* __restrict__ skip,
                                                unsigned e, unsigned H, unsigned W, int h, int w, int ac, float scale,
-                                               unsigned mW, unsigned mH) {
+                                               unsigned mW, unsigned mH, float usy, float usx) {
   const unsigned c4 = e & 15u;
   const unsigned p = e >> 4;
   const unsigned row = udiv_magic(p, W, mW);
   const int x = (int)(p - row * W);
   const unsigned b = udiv_magic(row, H, mH);
   const int y = (int)(row - b * H);
-  const UpIdx uy = up_index(y, h, (int)H, ac), ux = up_index(x, w, (int)W, ac);
+  const UpIdx uy = up2_index(y, h, (int)H, ac, usy), ux = up2_index(x, w, (int)W, ac, usx);
   const unsigned bb = b * (unsigned)h * (unsigned)w;
   const float4 a = s4[(bb + (unsigned)uy.i0 * w + ux.i0) * 16u + c4];
   const float4 bq = s4[(bb + (unsigned)uy.i0 * w + ux.i1) * 16u + c4];
   const float4 c = s4[(bb + (unsigned)uy.i1 * w + ux.i0) * 16u + c4];
   const float4 d = s4[(bb + (unsigned)uy.i1 * w + ux.i1) * 16u + c4];
   float4 v;
-  v.x = (a.x * ux.l0 + bq.x * ux.l1) * uy.l0 + (c.x * ux.l0 + d.x * ux.l1) * uy.l1;
-  v.y = (a.y * ux.l0 + bq.y * ux.l1) * uy.l0 + (c.y * ux.l0 + d.y * ux.l1) * uy.l1;
-  v.z = (a.z * ux.l0 + bq.z * ux.l1) * uy.l0 + (c.z * ux.l0 + d.z * ux.l1) * uy.l1;
-  v.w = (a.w * ux.l0 + bq.w * ux.l1) * uy.l0 + (c.w * ux.l0 + d.w * ux.l1) * uy.l1;
+  v.x = fvc_lerp2d(a.x, bq.x, c.x, d.x, ux.l0, ux.l1, uy.l0, uy.l1);
+  v.y = fvc_lerp2d(a.y, bq.y, c.y, d.y, ux.l0, ux.l1, uy.l0, uy.l1);
+  v.z = fvc_lerp2d(a.z, bq.z, c.z, d.z, ux.l0, ux.l1, uy.l0, uy.l1);
+  v.w = fvc_lerp2d(a.w, bq.w, c.w, d.w, ux.l0, ux.l1, uy.l0, uy.l1);
   if (scale != 1.f) { v.x *= scale; v.y *= scale; v.z *= scale; v.w *= scale; }
   if (skip) {
     float4 sk;
@@ -469,7 +481,8 @@ __device__ __forceinline__ float4 up2_q16_elem(const float4* __restrict__ s4, co
 
 template <int NE, bool NT>
 __global__ void k_up2_add_q16p(const float* __restrict__ src, const float* __restrict__ skip, float* __restrict__ out,
-                               int B, int h, int w, int ac, float scale, unsigned mW, unsigned mH) {
+                               int B, int h, int w, int ac, float scale, unsigned mW, unsigned mH, float usy,
+                               float usx) {
   const unsigned H = 2u * h, W = 2u * w;
   const unsigned n = (unsigned)B * H * W * 16u;
   const unsigned st = gridDim.x * blockDim.x;
@@ -480,7 +493,7 @@ __global__ void k_up2_add_q16p(const float* __restrict__ src, const float* __res
 #pragma unroll
     for (int k = 0; k < NE; ++k) {
       ei[k] = e + k * st < n ? e + k * st : e;
-      v[k] = up2_q16_elem<NT>(s4, skip, ei[k], H, W, h, w, ac, scale, mW, mH);
+      v[k] = up2_q16_elem<NT>(s4, skip, ei[k], H, W, h, w, ac, scale, mW, mH, usy, usx);
     }
 #pragma unroll
     for (int k = 0; k < NE; ++k) reinterpret_cast<float4*>(out)[ei[k]] = v[k];
@@ -488,7 +501,7 @@ __global__ void k_up2_add_q16p(const float* __restrict__ src, const float* __res
 }
 
 __global__ void k_up2_add(const float* __restrict__ src, const float* __restrict__ skip, float* __restrict__ out,
-                          int B, int h, int w, int cp, int ac, float scale) {
+                          int B, int h, int w, int cp, int ac, float scale, float usy, float usx) {
   const int H = 2 * h, W = 2 * w, c4n = cp / 4;
   const size_t n = (size_t)B * H * W * c4n;
   for (size_t e = grid_stride_start(); e < n; e += (size_t)gridDim.x * blockDim.x) {
@@ -497,7 +510,7 @@ __global__ void k_up2_add(const float* __restrict__ src, const float* __restrict
     const int x = p % W; p /= W;
     const int y = p % H;
     const size_t b = p / H;
-    const UpIdx uy = up_index(y, h, H, ac), ux = up_index(x, w, W, ac);
+    const UpIdx uy = up2_index(y, h, H, ac, usy), ux = up2_index(x, w, W, ac, usx);
     float4 v = up_sample4(src, b * h * w, w, c4n, c4, uy, ux);
     if (scale != 1.f) { v.x *= scale; v.y *= scale; v.z *= scale; v.w *= scale; }
     if (skip) {
@@ -576,8 +589,8 @@ __global__ void k_spynet_assemble_q(const float* __restrict__ im1, const float* 
     const float4 a = f4[bb + (unsigned)uy.i0 * w + ux.i0], bq = f4[bb + (unsigned)uy.i0 * w + ux.i1];
     const float4 c = f4[bb + (unsigned)uy.i1 * w + ux.i0], d = f4[bb + (unsigned)uy.i1 * w + ux.i1];
     float4 o;
-    o.x = (a.x * ux.l0 + bq.x * ux.l1) * uy.l0 + (c.x * ux.l0 + d.x * ux.l1) * uy.l1;
-    o.y = (a.y * ux.l0 + bq.y * ux.l1) * uy.l0 + (c.y * ux.l0 + d.y * ux.l1) * uy.l1;
+    o.x = fvc_lerp2d(a.x, bq.x, c.x, d.x, ux.l0, ux.l1, uy.l0, uy.l1);
+    o.y = fvc_lerp2d(a.y, bq.y, c.y, d.y, ux.l0, ux.l1, uy.l0, uy.l1);
     o.x = o.x * 2.f;
     o.y = o.y * 2.f;
     o.z = 0.f;
@@ -1465,6 +1478,9 @@ int fvc_upsample2x_add_nhwc(const float* src, const float* skip, float* out, int
   if (!src || !out || cp % 4) return FVC_EINVAL;
   const size_t n = (size_t)batch * 4 * h * w * (cp / 4);
   const unsigned long long H2 = 2ull * h, W2 = 2ull * w;
+  // align_corners scales (in - 1) / (out - 1), one host float division each (as ATen's CPU kernel)
+  const float usy = H2 > 1 ? (float)(h - 1) / (float)(H2 - 1) : 0.f;
+  const float usx = W2 > 1 ? (float)(w - 1) / (float)(W2 - 1) : 0.f;
   if (cp == 64 && (unsigned long long)batch * H2 * W2 * 16ull < (1ull << 32) && env_flag("FVC_UP2_Q16", 1)) {
     const unsigned mW = (unsigned)(((1ull << 32) + W2 - 1) / W2), mH = (unsigned)(((1ull << 32) + H2 - 1) / H2);
     // (index arithmetic e + 2 * stride stays below 2^32: stride <= 8192 * kBlk)
@@ -1473,16 +1489,16 @@ int fvc_upsample2x_add_nhwc(const float* src, const float* skip, float* out, int
     const bool nt = env_flag("FVC_UP2_NT", 1) != 0;
     if (n + (1ull << 24) < (1ull << 32) && env_flag("FVC_UP2_PAIR", 1) && nt)
       hipLaunchKernelGGL((k_up2_add_q16p<2, true>), dim3(grid_for((n + 1) / 2)), dim3(kBlk), 0, (hipStream_t)s, src, skip,
-                         out, batch, h, w, align_corners, scale, mW, mH);
+                         out, batch, h, w, align_corners, scale, mW, mH, usy, usx);
     else if (n + (1ull << 24) < (1ull << 32) && env_flag("FVC_UP2_PAIR", 1))
       hipLaunchKernelGGL((k_up2_add_q16p<2, false>), dim3(grid_for((n + 1) / 2)), dim3(kBlk), 0, (hipStream_t)s, src, skip,
-                         out, batch, h, w, align_corners, scale, mW, mH);
+                         out, batch, h, w, align_corners, scale, mW, mH, usy, usx);
     else
       hipLaunchKernelGGL(k_up2_add_q16, dim3(grid_for(n)), dim3(kBlk), 0, (hipStream_t)s, src, skip, out, batch, h, w,
-                         align_corners, scale, mW, mH);
+                         align_corners, scale, mW, mH, usy, usx);
   } else {
     hipLaunchKernelGGL(k_up2_add, dim3(grid_for(n)), dim3(kBlk), 0, (hipStream_t)s, src, skip, out, batch, h, w, cp,
-                       align_corners, scale);
+                       align_corners, scale, usy, usx);
   }
   FVC_CHECK_LAUNCH();
   return 0;

@@ -525,6 +525,42 @@ class PackedConv:
                                                                     4 * res[0].numel() if res is not None else 0)))
         return y, pool
 
+    def up_fusable(self) -> bool:
+        """The Winograd kernel can read skip + upsample(low) itself (fvc_conv2d_nhwc_wino_up);
+        FVC_UP_FUSE=0 keeps the standalone upsample-add kernel (A/B, tests)."""
+        return self.wino and self.tap is None and os.environ.get("FVC_UP_FUSE", "1") != "0"
+
+    def call_up(self, skip, low, in_op=IN_NONE, act=ACT_NONE):
+        """(conv(in_op(X)), X) with X = skip + upsample2x(low, bilinear, align_corners=True), X formed
+        in the conv's staging and written once (Warp_net c3_u / c4_u, endecoder.py:288-293); X is
+        bit-identical to upsample2x_add(low, skip)."""
+        if not self.up_fusable():
+            raise ValueError("conv cannot take the fused upsample-add input")
+        B, H, W, cp = skip.shape
+        if cp != cp4(self.cin) or H % 2 or W % 2:
+            raise ValueError(f"fused upsample-add input: skip {tuple(skip.shape)}")
+        _chk(skip, name="skip")
+        _chk(low, (B, H // 2, W // 2, cp), name="low")
+        xs = torch.empty_like(skip)
+        y = torch.empty((B, H, W, cp4(self.cout)), dtype=torch.float32, device=skip.device)
+        timer = profiling.active()
+        if timer is not None:
+            ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            ev0.record()
+        _lib.call("fvc_conv2d_nhwc_wino_up", skip.data_ptr(), low.data_ptr(), xs.data_ptr(), self.upack.data_ptr(),
+                  self.uosc, self.bias.data_ptr(), y.data_ptr(), B, H, W, in_op, act, _STATE["cu_reserve"],
+                  overflow_flag(skip.device).data_ptr(), sched_scratch(skip.device).data_ptr(), SCHED_LEN,
+                  stream_handle())
+        if timer is not None:
+            ev1.record()
+            # skip + low read, X and y written (the standalone upsample-add's traffic plus the conv's)
+            nbytes = 4 * (skip.numel() + low.numel() + xs.numel() + y.numel()) + \
+                self.wpack.numel() * self.wpack.element_size()
+            timer.records.append((ev0, ev1, profiling.conv_flops(self.cin, self.cout, self.ksize, 1, False, B, H, W),
+                                  f"conv{self.ksize}s1 {self.cin}->{self.cout} @{H}x{W} wino +up2add",
+                                  True, nbytes, "wino", 1))
+        return y, xs
+
     def _wino_tap(self, tap: "TapConsumer") -> bool:
         """The Winograd kernel's tap epilogue (fvc_conv2d_nhwc_wino_tap) takes this pair;
         FVC_WINO_TAP=0 keeps it on the direct kernel's (A/B, tests)."""

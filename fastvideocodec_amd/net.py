@@ -261,13 +261,24 @@ class Warp_net(nn.Module):
         c1, p1 = self.conv1.run_pool(p0)
         c2 = self.conv2.run(p1)
         c3 = self.conv3.run(c2)
-        c3u = K.upsample2x_add(c3, skip=c1, align_corners=True)
-        c4 = self.conv4.run(c3u)
-        c4u = K.upsample2x_add(c4, skip=c0, align_corners=True)
+        # c3_u = c1 + up(c3), c4_u = c0 + up(c4) (endecoder.py:288-293): formed inside the ResBlock
+        # conv1 that reads them (its staging), which also writes them for conv2's residual
+        y, c3u = self._conv1_up(self.conv4, c1, c3)
+        c4 = self.conv4.conv2.packed()(y, res=c3u)
+        y, c4u = self._conv1_up(self.conv5, c0, c4)
         # c5 = conv5(c4u) feeds only conv6 (64->3): its second conv runs fused with conv6's taps;
         # prediction = warpnet(...) + warpframe (net.py:67)
-        y = self.conv5.conv1.packed()(c4u, in_op=K.IN_RELU, act=K.ACT_RELU)
         return conv_then_tap(self.conv5.conv2, y, self.conv6, res=c4u, cons_res=warpframe)
+
+    @staticmethod
+    def _conv1_up(block, skip, low):
+        """(relu(conv1(relu(skip + up(low)))), skip + up(low)): one Winograd launch when the conv
+        takes the fused input, else the standalone upsample-add then conv1."""
+        p = block.conv1.packed()
+        if p.up_fusable():
+            return p.call_up(skip, low, in_op=K.IN_RELU, act=K.ACT_RELU)
+        xs = K.upsample2x_add(low, skip=skip, align_corners=True)
+        return p(xs, in_op=K.IN_RELU, act=K.ACT_RELU), xs
 
 
 class Analysis_net(nn.Module):

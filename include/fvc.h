@@ -157,6 +157,17 @@ int fvc_conv2d_nhwc_wino(const float* x, const void* wpack, float osc, const flo
                          const float* res, float* y, float* pool, int batch, int h, int w, int in_op,
                          int act, int cu_reserve, int* overflow_flag, int* sched, int sched_len,
                          fvc_stream_t stream);
+/* The same Winograd conv (in_op none / relu, act; no residual, pool or tap epilogue) reading
+ * X = skip + upsample(low, 2x, bilinear, align_corners=True) instead of a materialised input:
+ * Warp_net's c3_u = c1 + up(c3) and c4_u = c0 + up(c4) feeding ResBlock conv1
+ * (endecoder.py:288-293; replaces F.interpolate + add + the conv's input read). skip / xsum:
+ * [batch][h][w][64], low: [batch][h/2][w/2][64] (h, w even). X is formed in the kernel's LDS
+ * staging and also written to xsum (every pixel, bit-identical to fvc_upsample2x_add_nhwc with
+ * align_corners = 1, scale 1), which the ResBlock's conv2 reads as its residual. */
+int fvc_conv2d_nhwc_wino_up(const float* skip, const float* low, float* xsum, const void* wpack,
+                            float osc, const float* bias, float* y, int batch, int h, int w,
+                            int in_op, int act, int cu_reserve, int* overflow_flag, int* sched,
+                            int sched_len, fvc_stream_t stream);
 /* The same Winograd conv (in_op none, act, res) fused with the next layer's tap partials, as
  * fvc_conv2d_nhwc_x3_tap: instead of y it writes P [batch][h][w][pcp] = T . y per pixel (Warp_net
  * conv5.conv2 -> conv6, endecoder.py:278-279: 27 partials of the 64 -> 3 3x3 conv), which

@@ -252,3 +252,56 @@ def test_wino128_rejects_residual_and_wrong_pitch_forms():
     assert lib.fvc_conv_wino128_supported(128, 128, 3, 2, 0) == 0
     assert lib.fvc_conv_wino128_supported(64, 64, 3, 1, 0) == 0
     assert lib.fvc_conv2d_nhwc_wino128(None, None, None, None, None, 1, 4, 4, 0, 0, 0, None, None, 0, None) < 0
+
+
+# (B, H, W): the fused upsample-add input (Warp_net c3_u / c4_u feeding ResBlock conv1), sizes cut
+# at every edge: partial column groups, one tile row, several 16-row schedule chunks per column
+UP_CASES = [(1, 40, 72), (2, 36, 70), (1, 2, 30), (3, 68, 120), (1, 136, 96), (2, 4, 64)]
+
+
+@pytest.mark.parametrize("case", UP_CASES)
+def test_wino_up_fused_matches_upsample_then_conv(dev, case, monkeypatch):
+    """call_up (X = skip + up2(low) formed in the Winograd kernel's staging) against the
+    standalone upsample-add kernel followed by the plain Winograd launch: X and y bit for bit,
+    under the dynamic and the static chunk schedule, for the ResBlock conv1 form and a plain one;
+    the schedule scratch is left zeroed."""
+    B, H, W = case
+    g = torch.Generator().manual_seed(300 + H + W)
+    skip = to_nhwc(torch.randn(B, 64, H, W, generator=g)).to(dev)
+    low = to_nhwc(torch.randn(B, 64, H // 2, W // 2, generator=g)).to(dev)
+    w = torch.randn(64, 64, 3, 3, generator=g) * 0.05
+    b = torch.randn(64, generator=g) * 0.1
+    pw, _ = _packs(dev, w, b)
+    assert pw.up_fusable()
+    xs_ref = K.upsample2x_add(low, skip=skip, align_corners=True)
+    for in_op, act in ((K.IN_RELU, K.ACT_RELU), (K.IN_NONE, K.ACT_NONE)):
+        y_ref = pw(xs_ref, in_op=in_op, act=act)
+        y, xs = pw.call_up(skip, low, in_op=in_op, act=act)
+        monkeypatch.setenv("FVC_X3_DYN", "0")
+        y2, xs2 = pw.call_up(skip, low, in_op=in_op, act=act)
+        monkeypatch.delenv("FVC_X3_DYN")
+        torch.cuda.synchronize()
+        assert torch.equal(xs, xs_ref), float((xs - xs_ref).abs().max())
+        assert torch.equal(y, y_ref), float((y - y_ref).abs().max())
+        assert torch.equal(xs2, xs_ref) and torch.equal(y2, y_ref)
+    assert int(K.sched_scratch(dev)[:2].abs().sum()) == 0
+
+
+def test_wino_up_vs_float64(dev):
+    """The fused input against float64 torch: F.interpolate(low, 2x, bilinear, align_corners=True)
+    + skip, then the ResBlock conv1 (endecoder.py:228-293)."""
+    g = torch.Generator().manual_seed(31)
+    skip = torch.randn(2, 64, 68, 98, generator=g)
+    low = torch.randn(2, 64, 34, 49, generator=g)
+    w = torch.randn(64, 64, 3, 3, generator=g) * 0.05
+    b = torch.randn(64, generator=g) * 0.1
+    xr = skip.double() + F.interpolate(low.double(), scale_factor=2, mode="bilinear", align_corners=True)
+    ref = torch.relu(F.conv2d(torch.relu(xr), w.double(), b.double(), 1, 1))
+    pw, _ = _packs(dev, w, b)
+    y, xs = pw.call_up(to_nhwc(skip).to(dev), to_nhwc(low).to(dev), in_op=K.IN_RELU, act=K.ACT_RELU)
+    torch.cuda.synchronize()
+    ex = float((from_nhwc(xs.cpu()).double() - xr).abs().max())
+    ey = float((from_nhwc(y.cpu()).double() - ref).abs().max())
+    print(f"fused up: X err {ex:.2e} (scale {float(xr.abs().max()):.2f}), y err {ey / float(ref.abs().max()):.2e} of scale")
+    assert ex <= 4e-6 * float(xr.abs().max())
+    assert ey <= 2e-6 * float(ref.abs().max())
