@@ -441,6 +441,44 @@ __global__ __launch_bounds__(256, 1) void conv_wino_kernel(const WinoArgs a) {
   // horizontal lerp fmaf(b, l1x, a * l0x) is formed once for both rows: 4 low taps per column
   // instead of 8. Invalid entries (past the 544 (column slot, quad) pairs, outside the image) read
   // a safe address and write nothing.
+  // this lane's fix-up columns for column group g: (column slot, quad) pairs tid, tid + 256,
+  // tid + 512 (544 in all), their ring / xu offsets, low taps and weights. They depend on the group
+  // only, so they are formed when the fix-ups' group changes (once per chunk), not per item.
+  struct FixCols {
+    unsigned lo[3], xo[3];
+    int xa[3], xb[3];
+    float l0[3], l1[3];
+    bool ok[3], own[3];
+  };
+  auto fix_cols = [&](int g, int lc0) {
+    FixCols fc;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const int cmb0 = tid + 256 * j;
+      fc.ok[j] = cmb0 < 4 * 34 * 4;
+      const int cmb = fc.ok[j] ? cmb0 : tid;
+      const int qlo = cmb & 3, rest = cmb >> 2;
+      const int qhi = rest / 34, sl = rest - 34 * qhi;
+      const int q = 4 * qhi + qlo;
+      const int c = sl < 17 ? 2 * sl : 2 * (sl - 17) + 1;
+      const int ox = 32 * g - 1 + c;
+      fc.ok[j] = fc.ok[j] && (unsigned)ox < (unsigned)W;
+      fc.own[j] = c >= 1 && c <= 32;
+      const int oxc = min(max(ox, 0), W - 1);
+      const FvcUpIdx ux = fvc_up_index_scaled(oxc, a.wl, a.usx);
+      const int pa = ux.i0 - lc0, pb = ux.i1 - lc0;
+      fc.xa[j] = pa * kQ + (q ^ low_swz(pa));
+      fc.xb[j] = pb * kQ + (q ^ low_swz(pb));
+      fc.l0[j] = ux.l0;
+      fc.l1[j] = ux.l1;
+      fc.lo[j] = (unsigned)(q * kSlots + sl) * 16u;
+      fc.xo[j] = (unsigned)(oxc * kC + 4 * q) * 4u;
+    }
+    return fc;
+  };
+  FixCols fcols = {};
+  int fcols_g = -1;
+
   auto fixup_rows = [&](const Fix& f, int ri0) {
     bool rv[2], ro[2];
     int ya[2], yb[2];
@@ -462,29 +500,18 @@ __global__ __launch_bounds__(256, 1) void conv_wino_kernel(const WinoArgs a) {
     const __amdgpu_buffer_rsrc_t rxu = rsrc(a.xu + ((size_t)f.b * H + rxf) * W * kC, (unsigned)(min(H - rxf, 2) * W) * kC * 4u);
     const float4* const lw = reinterpret_cast<const float4*>(low);
     const bool shared = rv[0] && rv[1] && ya[0] == ya[1] && yb[0] == yb[1];  // wave-uniform
-    unsigned lo[3], xo[3];
-    bool ok[3], own[3];
+    const FixCols& fc = fcols;
+    const unsigned* const lo = fc.lo;
+    const unsigned* const xo = fc.xo;
+    const int* const xa = fc.xa;
+    const int* const xb = fc.xb;
+    const bool* const ok = fc.ok;
+    const bool* const own = fc.own;
     FvcUpIdx ux[3];
-    int xa[3], xb[3];
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
-      const int cmb0 = tid + 256 * j;
-      ok[j] = cmb0 < 4 * 34 * 4;
-      const int cmb = ok[j] ? cmb0 : tid;
-      const int qlo = cmb & 3, rest = cmb >> 2;
-      const int qhi = rest / 34, sl = rest - 34 * qhi;
-      const int q = 4 * qhi + qlo;
-      const int c = sl < 17 ? 2 * sl : 2 * (sl - 17) + 1;
-      const int ox = 32 * f.g - 1 + c;
-      ok[j] = ok[j] && (unsigned)ox < (unsigned)W;
-      own[j] = c >= 1 && c <= 32;
-      const int oxc = min(max(ox, 0), W - 1);
-      ux[j] = fvc_up_index_scaled(oxc, a.wl, a.usx);
-      const int pa = ux[j].i0 - f.lc0, pb = ux[j].i1 - f.lc0;
-      xa[j] = pa * kQ + (q ^ low_swz(pa));
-      xb[j] = pb * kQ + (q ^ low_swz(pb));
-      lo[j] = (unsigned)(q * kSlots + sl) * 16u;
-      xo[j] = (unsigned)(oxc * kC + 4 * q) * 4u;
+      ux[j].l0 = fc.l0[j];
+      ux[j].l1 = fc.l1[j];
     }
     char* const rw0 = ring + (size_t)((f.sbase + ri0) & (kRing - 1)) * kRowEntries * 16;
     char* const rw1 = ring + (size_t)((f.sbase + ri0 + 1) & (kRing - 1)) * kRowEntries * 16;
@@ -551,6 +578,10 @@ __global__ __launch_bounds__(256, 1) void conv_wino_kernel(const WinoArgs a) {
     if constexpr (FVC_UP_FORM == 1) {
       fixup_entry(f);
       return;
+    }
+    if (f.g != fcols_g) {  // wave-uniform: a new column group (at most once per chunk)
+      fcols = fix_cols(f.g, f.lc0);
+      fcols_g = f.g;
     }
     fixup_rows(f, 0);
     if (f.nr > 2) fixup_rows(f, 2);
