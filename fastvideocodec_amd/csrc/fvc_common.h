@@ -49,17 +49,16 @@ __device__ __forceinline__ float4 fvc_apply_in_op4(float4 v, int op) {
 // ------------------------------------------------------------------ bilinear upsampling (shared)
 // ATen compute_indices_weights_linear for align_corners=True with the scale (in-1)/(out-1)
 // precomputed (the caller computes it the same way: one correctly rounded float division), and the
-// bilinear combination in ATen's order (a l0x + b l1x) l0y + (c l0x + d l1x) l1y with explicit
-// fmaf, so the standalone upsample-add kernel (fvc_elem.hip) and the Winograd kernel's fused
-// upsample-add staging (fvc_conv_wino.hip) round identically.
+// bilinear combination in ATen's order (a l0x + b l1x) l0y + (c l0x + d l1x) l1y, every product and
+// sum rounded on its own (no contraction: the form the standalone upsample kernel has always
+// computed), so the standalone upsample-add kernel (fvc_elem.hip) and the Winograd kernel's fused
+// upsample-add staging (fvc_conv_wino.hip) produce the same bits.
 struct FvcUpIdx {
   int i0, i1;
   float l0, l1;
 };
 
 __device__ __forceinline__ FvcUpIdx fvc_up_index_scaled(int d, int in, float scale) {
-  // no contraction: src is rounded before the floor and the subtraction in every caller (with
-  // contraction the compiler may form lam = fma(scale, d, -i0) in one kernel and not in another)
 #pragma clang fp contract(off)
   const float src = scale * (float)d;
   int i0 = (int)floorf(src);
@@ -73,9 +72,15 @@ __device__ __forceinline__ FvcUpIdx fvc_up_index_scaled(int d, int in, float sca
   return u;
 }
 
+// one row's horizontal step a l0 + b l1 and the vertical step h0 l0y + h1 l1y (both unfused)
+__device__ __forceinline__ float fvc_lerp1(float a, float b, float l0, float l1) {
+#pragma clang fp contract(off)
+  return a * l0 + b * l1;
+}
+
 __device__ __forceinline__ float fvc_lerp2d(float a, float b, float c, float d, float l0x, float l1x, float l0y,
                                             float l1y) {
-  return fmaf(fmaf(d, l1x, c * l0x), l1y, fmaf(b, l1x, a * l0x) * l0y);
+  return fvc_lerp1(fvc_lerp1(a, b, l0x, l1x), fvc_lerp1(c, d, l0x, l1x), l0y, l1y);
 }
 
 __device__ __forceinline__ float4 fvc_lerp2d4(const float4& a, const float4& b, const float4& c, const float4& d,

@@ -438,7 +438,7 @@ __global__ __launch_bounds__(256, 1) void conv_wino_kernel(const WinoArgs a) {
   // and the low taps) is issued before the first result is formed, so the reads' latency is paid
   // once per pair of rows instead of once per entry. A fix-up's row pairs (2m + 1, 2m + 2) of a 2x
   // align_corners upsample share their two low rows (both floor to m); then (SHARED) each low row's
-  // horizontal lerp fmaf(b, l1x, a * l0x) is formed once for both rows: 4 low taps per column
+  // horizontal lerp a l0x + b l1x is formed once for both rows: 4 low taps per column
   // instead of 8. Invalid entries (past the 544 (column slot, quad) pairs, outside the image) read
   // a safe address and write nothing.
   // this lane's fix-up columns for column group g: (column slot, quad) pairs tid, tid + 256,
@@ -528,13 +528,13 @@ __global__ __launch_bounds__(256, 1) void conv_wino_kernel(const WinoArgs a) {
         }
       }
     };
-    auto hlerp = [&](const float4& ta, const float4& tb, const FvcUpIdx& u) {
-      return make_float4(fmaf(tb.x, u.l1, ta.x * u.l0), fmaf(tb.y, u.l1, ta.y * u.l0), fmaf(tb.z, u.l1, ta.z * u.l0),
-                         fmaf(tb.w, u.l1, ta.w * u.l0));
+    auto hlerp = [&](const float4& ta, const float4& tb, const FvcUpIdx& u) {  // fvc_lerp2d's inner steps
+      return make_float4(fvc_lerp1(ta.x, tb.x, u.l0, u.l1), fvc_lerp1(ta.y, tb.y, u.l0, u.l1),
+                         fvc_lerp1(ta.z, tb.z, u.l0, u.l1), fvc_lerp1(ta.w, tb.w, u.l0, u.l1));
     };
     auto vlerp = [&](const float4& h0, const float4& h1, int k) {  // = fvc_lerp2d's outer step
-      return make_float4(fmaf(h1.x, ly1[k], h0.x * ly0[k]), fmaf(h1.y, ly1[k], h0.y * ly0[k]),
-                         fmaf(h1.z, ly1[k], h0.z * ly0[k]), fmaf(h1.w, ly1[k], h0.w * ly0[k]));
+      return make_float4(fvc_lerp1(h0.x, h1.x, ly0[k], ly1[k]), fvc_lerp1(h0.y, h1.y, ly0[k], ly1[k]),
+                         fvc_lerp1(h0.z, h1.z, ly0[k], ly1[k]), fvc_lerp1(h0.w, h1.w, ly0[k], ly1[k]));
     };
     if (shared) {
       float4 t[3][6];  // two entries, then the four taps
