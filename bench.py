@@ -711,6 +711,10 @@ def roofline_fields(prof, job, args):
                      "frac_of_x3_ceiling": round(achieved / (F16_MFMA_PEAK_TFLOPS / 3), 4),
                      **issued_fields(prof, x3_ms),
                      "per_kernel": per_kernel_fields(prof, nfr),
+                     "fused_hbm_work": "since r6 the Warp_net upsample-adds (c3_u = c1 + up(c3), c4_u = c0 + "
+                                       "up(c4), endecoder.py:288-293; 0.63 ms per P-frame as a standalone HBM kernel "
+                                       "in r5) are formed inside the ResBlock conv1 Winograd launches that read them: "
+                                       "their time is in this family's and their bytes in algorithmic_bytes_per_launch",
                      "measured": "HIP events on the launching stream around every conv launch of one serial GOP",
                      "launches": x3_launch, "ms_per_pframe": round(x3_ms / nfr, 3),
                      "gflop_per_pframe": round(x3_flops / nfr / 1e9, 1),
@@ -771,8 +775,25 @@ def per_kernel_fields(prof, nfr):
                      "ms_per_pframe": round(ms / nfr, 3), "gflop_per_pframe": round(fl / nfr / 1e9, 1),
                      "algorithmic_gbps": round(nbytes / (ms * 1e-3) / 1e9, 1),
                      "f16_mfma_tflops_issued": round(ISSUED_PER_FLOP[fam] * tf, 1),
-                     "frac_of_f16_peak_issued": round(ISSUED_PER_FLOP[fam] * tf / F16_MFMA_PEAK_TFLOPS, 4)}
+                     "frac_of_f16_peak_issued": round(ISSUED_PER_FLOP[fam] * tf / F16_MFMA_PEAK_TFLOPS, 4),
+                     **attainable_fields(tf, nbytes / (ms * 1e-3), fam)}
     return out
+
+
+def attainable_fields(tflops, bytes_per_s, fam):
+    """The roofline model for one kernel family: attainable = min(its MFMA ceiling (f16 peak / the
+    f16 FLOP it issues per algorithmic FLOP), arithmetic intensity (algorithmic FLOP per algorithmic
+    byte) x 8 TB/s); `bound` names the smaller. The Winograd family's intensity is low enough
+    (~120-140 FLOP per byte against a ~230 ridge for its ceiling) that HBM bounds it."""
+    if bytes_per_s <= 0:
+        return {}
+    ai = tflops * 1e12 / bytes_per_s
+    mfma_ceiling = F16_MFMA_PEAK_TFLOPS / ISSUED_PER_FLOP[fam]
+    hbm_ceiling = ai * HBM_PEAK_BPS / 1e12
+    att = min(mfma_ceiling, hbm_ceiling)
+    return {"flop_per_byte": round(ai, 1), "frac_of_8tbps": round(bytes_per_s / HBM_PEAK_BPS, 4),
+            "attainable_tflops": round(att, 1), "attainable_bound": "hbm" if hbm_ceiling < mfma_ceiling else "mfma",
+            "frac_of_attainable": round(tflops / att, 4)}
 
 
 def load_pmc_traffic(H, W, gops):

@@ -31,9 +31,11 @@
 // Input: a ring of 8 raw fp32 input rows in LDS filled by LDS-DMA (buffer_load_dwordx4 ... lds, one
 // descriptor per row: padding rows and columns read past it and land as zeros); consecutive items of a block walk down one tile column, so each item
 // stages the 2 new rows of its 4-row window while the previous item computes.
-// LDS input layout: row slot -> 16 channel quads -> 40 column slots of 16 B, even columns 0..16 then
-// odd columns 17..33 (the tile columns of a patch are 2 apart): a lane group's ds_read_b128 of 16
-// tiles x 2 octets covers all 64 banks once.
+// LDS input layout (r6): row slot -> 34 columns -> 16 channel quads, the quad index XORed with
+// (column >> 1) & 15 (ring_entry): the LDS image of a row is its 34 pixels as they lie in memory, up
+// to that swizzle, so each LDS-DMA instruction reads 4 whole pixels (1 KB contiguous), and the
+// transform's ds_read_b128 of 16 tiles (columns 2t + d) x a quad still covers every bank group
+// once per 16 lanes. (r3-r5: quad-major lines with even / odd column halves; -DFVC_WINO_PIX=0.)
 // Epilogue forms: plain (bias, ReLU / LeakyReLU, residual add), and POOL, which also writes the
 // 2x2 average pool of the output (each pool window is one Winograd tile: ATen's ((x00 + x01) + x10)
 // + x11) / 4, bit-identical to k_avgpool2).
@@ -59,13 +61,23 @@ constexpr int kC = 64;             // input and output channels
 constexpr int kQ = kC / 4;         // channel quads per pixel
 constexpr int kTiles = 16;         // tiles per item: one tile row x 16 tile columns
 constexpr int kCols = 2 * kTiles + 2;  // input columns an item reads
-constexpr int kSlots = 40;         // column slots per (row, quad) line (34 used)
-constexpr int kRowEntries = kQ * kSlots;   // 16-B entries per staged row (640)
+// staged-row layout. FVC_WINO_PIX 1 (default, r6): pixel-major, entry (local column c, quad Q) at
+// c * 16 + (Q ^ ((c >> 1) & 15)), 34 columns padded to 36 (9 LDS-DMA pieces): every DMA instruction
+// reads 4 whole pixels (1 KB of consecutive bytes). 0 (r3-r5): quad-major, even columns in slots
+// 0..16 and odd ones in 17..33 of a 40-slot line per quad: each DMA instruction gathered 16 B from
+// ~40 pixels. Both give conflict-free ds_read_b128 for the transform's reads (16 tiles x a quad).
+#ifndef FVC_WINO_PIX
+#define FVC_WINO_PIX 1
+#endif
+constexpr bool kPix = FVC_WINO_PIX != 0;
+constexpr int kSlots = 40;         // quad-major form: column slots per (row, quad) line (34 used)
+constexpr int kRowEntries = kPix ? 36 * kQ : kQ * kSlots;   // 16-B entries per staged row (576 / 640)
+constexpr int kRowPieces = kRowEntries / 64;                // LDS-DMA pieces per row (9 / 10)
 constexpr int kRing = 8;           // staged input rows
-constexpr int kRingBytes = kRing * kRowEntries * 16;  // 81920
+constexpr int kRingBytes = kRing * kRowEntries * 16;  // 73,728 (quad-major: 81,920)
 constexpr int kZBytes = 4 * 8 * 1024;                 // one Z buffer: 4 waves x 8 planes x 1 KB
 constexpr int kHdr = 512;                             // bias (256 B) + schedule words
-constexpr int kLds = kHdr + kRingBytes + 2 * kZBytes; // 148,480 B
+constexpr int kLds = kHdr + kRingBytes + 2 * kZBytes; // 139,776 B (quad-major: 148,480)
 // fused upsample-add input (UP): the low-resolution rows one item's fix-up reads, [row][pixel][quad]
 // (up to 4 source rows x 20 source columns, the span 4 output rows x 34 output columns of a 2x
 // align_corners=True upsample can reach); Z single-buffered (two barriers per item)
@@ -73,7 +85,7 @@ constexpr int kLowRows = 4;
 constexpr int kLowCols = 20;
 constexpr int kLowRowEnt = kLowCols * kQ;                  // 16-B entries per low row (320)
 constexpr int kLowBytes = kLowRows * kLowRowEnt * 16;      // 20,480
-constexpr int kLdsUp = kHdr + kRingBytes + kZBytes + kLowBytes;  // 135,680 B
+constexpr int kLdsUp = kHdr + kRingBytes + kZBytes + kLowBytes;  // 127,488 B
 constexpr int kChunk = 16;         // items per schedule chunk (consecutive tile rows of one column)
 constexpr float kLoScale = 2048.f;
 // knock-outs (experiment builds only; results wrong): FVC_WINO_KO bit 1 = no k-step-1 MFMAs,
@@ -138,6 +150,12 @@ struct WinoArgs {
 };
 
 typedef __attribute__((address_space(3))) void* lds_ptr;
+
+// 16-B entry of (local column c = 0..33, channel quad Q) within a staged row
+__device__ __forceinline__ int ring_entry(int c, int Q) {
+  if constexpr (kPix) return c * kQ + (Q ^ ((c >> 1) & 15));
+  return Q * kSlots + ((c & 1) ? 17 + (c >> 1) : (c >> 1));
+}
 
 // UP: quad swizzle of the low rows' LDS image (pixel p's quad q at slot q ^ low_swz(p))
 __device__ __forceinline__ int low_swz(int p) { return (p & 3) << 2; }
@@ -265,6 +283,10 @@ __global__ __launch_bounds__(256, 1) void conv_wino_kernel(const WinoArgs a) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // = row r of the transform domain
   const int t = lane & 15;    // tile of this lane (MFMA B column / D column)
   const int o = lane >> 4;    // channel octet of this lane within a 32-channel k-step
+  // kPix: byte offset of column 2t in a staged row, and the quad swizzles of columns 2t, 2t + 1
+  // ((2t >> 1) & 15 = t) and 2t + 2, 2t + 3 ((t + 1) & 15), each XORed with the octet's 2 o, x 16 B
+  const int pix_b = 2 * t * kQ * 16;
+  const int pix_x0 = ((2 * o) ^ t) * 16, pix_x1 = ((2 * o) ^ ((t + 1) & 15)) * 16;
   const int W = a.W, H = a.H;
 
   // resident U: u[q][n][kk][plane], 4 registers each (AGPRs: the MFMA asm's "a" operands)
@@ -295,11 +317,17 @@ __global__ __launch_bounds__(256, 1) void conv_wino_kernel(const WinoArgs a) {
 #pragma unroll
   for (int m = 0; m < 3; ++m) {
     const int e = (wave + 4 * m) * 64 + lane;
-    const int c4 = e / kSlots, cs = e - c4 * kSlots;
-    dma_lc[m] = cs < 17 ? 2 * cs : (cs < 34 ? 2 * (cs - 17) + 1 : -(1 << 20));
-    dma_ch[m] = 4 * c4;
+    if constexpr (kPix) {
+      const int c = e >> 4, qq = e & 15;
+      dma_lc[m] = c < 34 ? c : -(1 << 20);
+      dma_ch[m] = 4 * (qq ^ ((c >> 1) & 15));
+    } else {
+      const int c4 = e / kSlots, cs = e - c4 * kSlots;
+      dma_lc[m] = cs < 17 ? 2 * cs : (cs < 34 ? 2 * (cs - 17) + 1 : -(1 << 20));
+      dma_ch[m] = 4 * c4;
+    }
   }
-  const int npiece = wave < 2 ? 3 : 2;  // 10 pieces over 4 waves
+  const int npiece = wave < kRowPieces - 8 ? 3 : 2;  // 9 / 10 pieces over 4 waves
   // byte offsets of the lane's pieces within an input row of column group g (past the row for
   // padding columns and pad slots: the buffer unit returns zeros)
   auto row_offsets = [&](int g, unsigned (&vo)[3]) {
@@ -419,7 +447,7 @@ __global__ __launch_bounds__(256, 1) void conv_wino_kernel(const WinoArgs a) {
         const FvcUpIdx uy = fvc_up_index_scaled(r, a.hl, a.usy);
         const int ya = (uy.i0 - f.lr0) * kLowRowEnt, yb = (uy.i1 - f.lr0) * kLowRowEnt;
         float4* const pe =
-            reinterpret_cast<float4*>(ring + ((size_t)((f.sbase + ri) & (kRing - 1)) * kRowEntries + q * kSlots + sl) * 16);
+            reinterpret_cast<float4*>(ring + ((size_t)((f.sbase + ri) & (kRing - 1)) * kRowEntries + ring_entry(c, q)) * 16);
         const float4* const lw = reinterpret_cast<const float4*>(low);
         const float4 sk = *pe;
         const float4 v = fvc_lerp2d4(lw[ya + xa], lw[ya + xb], lw[yb + xa], lw[yb + xb], uy, ux);
@@ -471,7 +499,7 @@ __global__ __launch_bounds__(256, 1) void conv_wino_kernel(const WinoArgs a) {
       fc.xb[j] = pb * kQ + (q ^ low_swz(pb));
       fc.l0[j] = ux.l0;
       fc.l1[j] = ux.l1;
-      fc.lo[j] = (unsigned)(q * kSlots + sl) * 16u;
+      fc.lo[j] = (unsigned)ring_entry(c, q) * 16u;
       fc.xo[j] = (unsigned)(oxc * kC + 4 * q) * 4u;
     }
     return fc;
@@ -703,16 +731,28 @@ __global__ __launch_bounds__(256, 1) void conv_wino_kernel(const WinoArgs a) {
       // software-pipelined: the next k-step's LDS reads and transform sit between this k-step's
       // MFMA blocks (source order is issue order around the asm blocks)
       auto read_raw = [&](int kk, int hh, float4 (&da)[4], float4 (&db)[4]) {
+        (void)pix_b;
         // patch columns 0..3 of tile t: slots t, 17 + t, t + 1, 18 + t (even / odd column halves)
-        const int e0 = ((8 * kk + 2 * o + hh) * kSlots + t) * 16;
-        da[0] = *reinterpret_cast<const float4*>(rowa + e0);
-        da[1] = *reinterpret_cast<const float4*>(rowa + e0 + 17 * 16);
-        da[2] = *reinterpret_cast<const float4*>(rowa + e0 + 16);
-        da[3] = *reinterpret_cast<const float4*>(rowa + e0 + 18 * 16);
-        db[0] = *reinterpret_cast<const float4*>(rowb + e0);
-        db[1] = *reinterpret_cast<const float4*>(rowb + e0 + 17 * 16);
-        db[2] = *reinterpret_cast<const float4*>(rowb + e0 + 16);
-        db[3] = *reinterpret_cast<const float4*>(rowb + e0 + 18 * 16);
+        const int Q = 8 * kk + 2 * o + hh;
+        int e[4];
+        if constexpr (kPix) {  // = ring_entry(2t + d, Q) * 16: (8 kk + hh) ^ (2 o ^ swizzle), per-lane parts hoisted
+          const int cq = (8 * kk + hh) * 16;
+          e[0] = pix_b + (cq ^ pix_x0);
+          e[1] = e[0] + 256;
+          e[2] = pix_b + 512 + (cq ^ pix_x1);
+          e[3] = e[2] + 256;
+        } else {
+          const int e0 = (Q * kSlots + t) * 16;
+          e[0] = e0;
+          e[1] = e0 + 17 * 16;
+          e[2] = e0 + 16;
+          e[3] = e0 + 18 * 16;
+        }
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+          da[d] = *reinterpret_cast<const float4*>(rowa + e[d]);
+          db[d] = *reinterpret_cast<const float4*>(rowb + e[d]);
+        }
       };
       // V[q] = E B of the lane's tile for 4 channels (E = d[ra] + sb d[rb]), two channels per packed
       // instruction (v_pk_fma_f32 / v_pk_add_f32; a lone wave issues one VALU per ~4 cycles whether
