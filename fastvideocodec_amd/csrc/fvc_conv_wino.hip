@@ -86,7 +86,8 @@ constexpr int kLowCols = 20;
 constexpr int kLowRowEnt = kLowCols * kQ;                  // 16-B entries per low row (320)
 constexpr int kLowBytes = kLowRows * kLowRowEnt * 16;      // 20,480
 constexpr int kLdsUp = kHdr + kRingBytes + kZBytes + kLowBytes;  // 127,488 B
-constexpr int kChunk = 16;         // items per schedule chunk (consecutive tile rows of one column)
+// items per schedule chunk (consecutive tile rows of one column): 16 (32 as an experiment switch)
+constexpr int kChunkMin = 16, kChunkMax = 32;
 constexpr float kLoScale = 2048.f;
 // knock-outs (experiment builds only; results wrong): FVC_WINO_KO bit 1 = no k-step-1 MFMAs,
 // 2 = no k-step-0 MFMAs (their split VALU kept), 4 = no item barrier, 8 = no finishing pass,
@@ -128,7 +129,7 @@ struct WinoArgs {
   float* pool;
   int B, H, W;
   int tiles_y, ngroups;  // tile rows, 32-column groups
-  int nchunks, chunks_per_col;
+  int nchunks, chunks_per_col, chunk;  // chunk: items (tile rows) per schedule chunk
   float osc, osc_c;      // 2^-kw, 2^-kw-11
   int* sched;            // [0] blocks finished, [1] next chunk; zero on entry, reset by the last block
   int* ovf;
@@ -369,8 +370,8 @@ __global__ __launch_bounds__(256, 1) void conv_wino_kernel(const WinoArgs a) {
     Pos p{0, 0, 0, 0};
     if (ch < a.nchunks) {
       const int col = ch / a.chunks_per_col;
-      p.ty0 = (ch - col * a.chunks_per_col) * kChunk;
-      p.ty1 = min(p.ty0 + kChunk, a.tiles_y);
+      p.ty0 = (ch - col * a.chunks_per_col) * a.chunk;
+      p.ty1 = min(p.ty0 + a.chunk, a.tiles_y);
       p.b = col / a.ngroups;
       p.g = col - p.b * a.ngroups;
     }
@@ -1107,7 +1108,12 @@ static int run_wino(const float* x, const void* upack, float osc, const float* b
   a.W = w;
   a.tiles_y = (h + 1) / 2;
   a.ngroups = fvc_cdiv(w, 32);
-  a.chunks_per_col = fvc_cdiv(a.tiles_y, kChunk);
+  // 16 tile rows per chunk. Longer chunks re-stage fewer halo rows (a chunk's first item stages 4
+  // rows, later ones 2): FVC_WINO_CHUNK=32 (experiments) measured equal on the 1088x1920 and
+  // 544x960 layers and 4-5 % slower on the 272x480 quarters (profiles/r6/wino_ko/chunk.txt).
+  // The result does not depend on it.
+  a.chunk = env_int("FVC_WINO_CHUNK", kChunkMin) == kChunkMax ? kChunkMax : kChunkMin;
+  a.chunks_per_col = fvc_cdiv(a.tiles_y, a.chunk);
   a.nchunks = batch * a.ngroups * a.chunks_per_col;
   a.osc = osc;
   a.osc_c = osc * (1.0f / 2048.f);
