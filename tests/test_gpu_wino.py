@@ -255,8 +255,9 @@ def test_wino128_rejects_residual_and_wrong_pitch_forms():
 
 
 # (B, H, W): the fused upsample-add input (Warp_net c3_u / c4_u feeding ResBlock conv1), sizes cut
-# at every edge: partial column groups, one tile row, several 16-row schedule chunks per column
-UP_CASES = [(1, 40, 72), (2, 36, 70), (1, 2, 30), (3, 68, 120), (1, 136, 96), (2, 4, 64)]
+# at every edge: partial column groups, one tile row, several 16-row schedule chunks per column,
+# chunks of 1, 2 and 4 items (the staging two items ahead falls back at chunk ends)
+UP_CASES = [(1, 40, 72), (2, 36, 70), (1, 2, 30), (3, 68, 120), (1, 136, 96), (2, 4, 64), (2, 34, 66), (1, 66, 40)]
 
 
 @pytest.mark.parametrize("case", UP_CASES)
