@@ -105,6 +105,9 @@ constexpr float kLoScale = 2048.f;
 #ifndef FVC_UP_FORM
 #define FVC_UP_FORM 0
 #endif
+#ifndef FVC_UP_FIRST
+#define FVC_UP_FIRST 0
+#endif
 #ifndef FVC_WINO_KO_WAIT
 #define FVC_WINO_KO_WAIT 0
 #endif
@@ -875,6 +878,7 @@ __global__ __launch_bounds__(256, 1) void conv_wino_kernel(const WinoArgs a) {
 #endif
       if constexpr (!(FVC_WINO_KO & 4)) __syncthreads();
       if (first) nnp = decode(sq[2 + (ntaken & 1)]);  // published by this item's barrier
+      if constexpr (UP && FVC_UP_FIRST) fixup(nf);  // experiment: the fix-up before the finishing pass
 
       // ---- finishing pass: wave w -> output channels 16w..16w+15 of the item's 16 tiles
       if constexpr (!(FVC_WINO_KO & 8)) {
@@ -984,7 +988,7 @@ __global__ __launch_bounds__(256, 1) void conv_wino_kernel(const WinoArgs a) {
       }  // FVC_WINO_KO & 8
 
       if constexpr (UP) {  // the next item's new rows: S -> X in place (and to xu), then published
-        fixup(nf);
+        if constexpr (!FVC_UP_FIRST) fixup(nf);
         if constexpr (!(FVC_UP_KO & 2)) __syncthreads();
       }
 
