@@ -711,6 +711,7 @@ def roofline_fields(prof, job, args):
                      "frac_of_x3_ceiling": round(achieved / (F16_MFMA_PEAK_TFLOPS / 3), 4),
                      **issued_fields(prof, x3_ms),
                      "per_kernel": per_kernel_fields(prof, nfr),
+                     "dominant_kernel": dominant_kernel_fields(per_kernel_fields(prof, nfr)),
                      "fused_hbm_work": "since r6 the Warp_net upsample-adds (c3_u = c1 + up(c3), c4_u = c0 + "
                                        "up(c4), endecoder.py:288-293; 0.63 ms per P-frame as a standalone HBM kernel "
                                        "in r5) are formed inside the ResBlock conv1 Winograd launches that read them: "
@@ -778,6 +779,26 @@ def per_kernel_fields(prof, nfr):
                      "frac_of_f16_peak_issued": round(ISSUED_PER_FLOP[fam] * tf / F16_MFMA_PEAK_TFLOPS, 4),
                      **attainable_fields(tf, nbytes / (ms * 1e-3), fam)}
     return out
+
+
+def dominant_kernel_fields(pk):
+    """The family member with the most time per P-frame, on the roofline its own arithmetic
+    intensity puts it on (attainable_fields): for the Winograd kernel HBM, so achieved / peak are
+    algorithmic GB/s / 8 TB/s. The family's `frac` above stays the MFMA-peak framing."""
+    if not pk:
+        return None
+    name, v = max(pk.items(), key=lambda kv: kv[1]["ms_per_pframe"])
+    if v.get("attainable_bound") == "hbm":
+        achieved, peak, unit = v["algorithmic_gbps"], HBM_PEAK_BPS / 1e9, "GB/s"
+    else:
+        achieved, peak, unit = v["achieved"], F16_MFMA_PEAK_TFLOPS / ISSUED_PER_FLOP[FAMILY_OF[name]], "TFLOP/s"
+    return {"kernel": name, "bound": v.get("attainable_bound"), "achieved": achieved, "peak": round(peak, 1),
+            "unit": unit, "frac": round(achieved / peak, 4) if peak else None,
+            "flop_per_byte": v.get("flop_per_byte"), "ms_per_pframe": v["ms_per_pframe"]}
+
+
+FAMILY_OF = {"conv_x3_kernel": "x3", "conv_dx_kernel": "dx", "conv_wino_kernel": "wino", "conv_wr7_kernel": "wr7",
+             "conv_stem_kernel": "stem"}
 
 
 def attainable_fields(tflops, bytes_per_s, fam):
