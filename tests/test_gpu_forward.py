@@ -223,6 +223,28 @@ def test_batch_matches_single(model, dev):
     assert torch.equal(two[0:1], one) and torch.equal(two[1:2], one)
 
 
+def test_fused_upsample_add_leaves_forward_bitexact(model, dev, monkeypatch):
+    """Warp_net's upsample-adds formed inside ResBlock conv1 (fvc_conv2d_nhwc_wino_up, the default)
+    against the standalone upsample-add kernel then conv1 (FVC_UP_FUSE=0): the whole 8-tuple of
+    VideoCompressor.forward (net.py:70-220) and the prediction are bit-identical, at 256x256 and at
+    192x320 x 2 frames (the quarter-resolution ResBlocks' 80 columns cut a column group; several
+    schedule chunks per column)."""
+    g = np.load(os.path.join(GOLD, "dvc_256x256.npz"))
+    pairs = [(torch.from_numpy(g["input_image"]).to(dev), torch.from_numpy(g["referframe"]).to(dev))]
+    gen = torch.Generator().manual_seed(17)
+    pairs.append((torch.rand(2, 3, 192, 320, generator=gen).to(dev), torch.rand(2, 3, 192, 320, generator=gen).to(dev)))
+    for cur, ref in pairs:
+        monkeypatch.setenv("FVC_UP_FUSE", "1")
+        a, ta = model(cur, ref, return_intermediates=True)
+        monkeypatch.setenv("FVC_UP_FUSE", "0")
+        b, tb = model(cur, ref, return_intermediates=True)
+        monkeypatch.delenv("FVC_UP_FUSE")
+        torch.cuda.synchronize()
+        for x, y in zip(a, b):
+            assert torch.equal(torch.as_tensor(x), torch.as_tensor(y))
+        assert torch.equal(ta["prediction"], tb["prediction"])
+
+
 def test_rejects_bad_sizes(model, dev):
     x = torch.rand(1, 3, 100, 64, device=dev)
     with pytest.raises(ValueError):
