@@ -422,14 +422,14 @@ class PackedConv:
             ev0.record()
         wino = self.wino and in_op in (IN_NONE, IN_RELU) and post == POST_NONE
         # the quarters pay 4 launch tails: at 16 GOPs per launch 136x240 0.58 -> 0.62 ms, 272x480
-        # 1.97 -> 1.72, 544x960 7.46 -> 6.08 (MI355X, profiles/r3/wino128); images of >= 100 K
-        # pixels (544x960 and 272x480) take them. r3 measured the 100 K gate bench-neutral against
-        # 200 K (70.91 / 70.96 vs 71.08 / 70.89); r5, with the rest of the step faster, +0.8 %
-        # (78.55 / 78.49 vs 77.87 / 77.97, interleaved runs on one box, profiles/r5/gate_100k).
-        # Gated per image, not per launch: a frame's result must not depend on how many frames
-        # share its batch.
+        # 1.97 -> 1.72, 544x960 7.46 -> 6.08 (MI355X, profiles/r3/wino128). r3 measured a 100 K gate
+        # bench-neutral against 200 K; r5 +0.8 % (profiles/r5/gate_100k); r6, with the faster
+        # pixel-major Winograd rows, 200 K / 100 K / 30 K = 80.3 / 81.0-81.1 / 81.3-81.4 P-frames/s
+        # (interleaved, profiles/r6/gate_wino128): images of >= 30 K pixels (544x960, 272x480 and
+        # 136x240) take them. Gated per image, not per launch: a frame's result must not depend on
+        # how many frames share its batch.
         w128 = (self.wino128 and in_op in (IN_NONE, IN_RELU) and post == POST_NONE and res is None and
-                H * W >= int(os.environ.get("FVC_WINO128_MINPIX", "100000")))
+                H * W >= int(os.environ.get("FVC_WINO128_MINPIX", "30000")))
         wr7 = bool(self.wr7) and in_op == IN_NONE and post == POST_NONE and res is None
         stem = self.stem is not None and in_op == IN_NONE and post == POST_NONE and res is None
         if stem:
